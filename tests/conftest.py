@@ -1,0 +1,22 @@
+import os
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO))
+GOLDEN = REPO / "tests" / "golden"
+FIXTURE = REPO / "tests" / "fixture"
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libs3od_hip.so)")
+    config.addinivalue_line("markers", "slow: long-running test")
+
+
+@pytest.fixture(scope="session")
+def synth_sd_torch():
+    import torch
+    from s3od_amd.weights import synthetic_state_dict
+    return {k: torch.from_numpy(v) for k, v in synthetic_state_dict(0).items()}
