@@ -1,0 +1,79 @@
+// Shared device/host helpers for libs3od_hip (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+typedef __bf16 bf16;
+typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+// dtype enum shared with include/s3od_hip.h
+enum { S3OD_F32 = 0, S3OD_BF16 = 1 };
+
+#define DEV __device__ __forceinline__
+
+// ------------------------------------------------------------------ error reporting
+void s3od_set_error(const char* fmt, ...);
+int s3od_check_launch(const char* what);
+
+#define S3OD_REQUIRE(cond, ...)                     \
+  do {                                              \
+    if (!(cond)) {                                  \
+      s3od_set_error(__VA_ARGS__);                  \
+      return 22; /* EINVAL-like, distinct from hipError codes used below */ \
+    }                                               \
+  } while (0)
+
+// ------------------------------------------------------------------ conversions
+template <typename T> DEV float to_f(T v);
+template <> DEV float to_f<float>(float v) { return v; }
+template <> DEV float to_f<bf16>(bf16 v) { return (float)v; }
+template <typename T> DEV T from_f(float v);
+template <> DEV float from_f<float>(float v) { return v; }
+template <> DEV bf16 from_f<bf16>(float v) { return (bf16)v; }
+
+// 8 consecutive elements <-> floats (16 B for bf16, 32 B for f32)
+template <typename T> DEV void load8(const T* p, float* v);
+template <> DEV void load8<float>(const float* p, float* v) {
+  float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+template <> DEV void load8<bf16>(const bf16* p, float* v) {
+  bf16x8 a = *(const bf16x8*)p;
+#pragma unroll
+  for (int i = 0; i < 8; i++) v[i] = (float)a[i];
+}
+template <typename T> DEV void store8(T* p, const float* v);
+template <> DEV void store8<float>(float* p, const float* v) {
+  *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+template <> DEV void store8<bf16>(bf16* p, const float* v) {
+  bf16x8 a;
+#pragma unroll
+  for (int i = 0; i < 8; i++) a[i] = (bf16)v[i];
+  *(bf16x8*)p = a;
+}
+
+DEV float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+DEV float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+DEV float gelu_erf_grad(float x) {
+  float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

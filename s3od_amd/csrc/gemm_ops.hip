@@ -1,0 +1,276 @@
+// C-ABI entry points built on the implicit-GEMM engine (gemm.hpp).
+#include "gemm.hpp"
+#include <type_traits>
+
+#define DISPATCH_T(dtype, ...)                                                  \
+  do {                                                                          \
+    if ((dtype) == S3OD_BF16) { typedef bf16 T; __VA_ARGS__ }                   \
+    else if ((dtype) == S3OD_F32) { typedef float T; __VA_ARGS__ }              \
+    else { s3od_set_error("bad dtype %d", (int)(dtype)); return 22; }           \
+  } while (0)
+
+static RowMap dense_rm() { RowMap r{}; r.mode = 0; return r; }
+
+// ------------------------------------------------------------------ QKV + RoPE epilogue
+// n in [0,2304): q | k | v ; RoPE on patch tokens for q,k (tf:…/modeling_dinov3_vit.py:238-268);
+// q pre-multiplied by the softmax scale 1/8 (exact in any binary float format).
+template <typename T> struct EpiQKV {
+  T* q; T* k; T* v; const float* bias; const float* cs; const float* sn;
+  int M, Ntok, P, H;
+  DEV void prepare(int) {}
+  DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN) const {
+    for_segments(ct, LDT, BM, BN, m0, n0, M, 3 * H * 64, tid, [&](int m, int n, const float* a, int r, int c) {
+      int which = n / (H * 64), nn = n - which * H * 64, h = nn >> 6, d0 = nn & 63;
+      int b = m / Ntok, t = m - b * Ntok;
+      float val[8];
+#pragma unroll
+      for (int e = 0; e < 8; e++) val[e] = a[e] + (bias ? bias[n + e] : 0.f);
+      if (which < 2 && t >= Ntok - P) {
+        int dc = d0 < 32 ? 32 : -32;
+        const float* pa = ct + r * LDT + c + dc;
+        int tp = t - (Ntok - P);
+        const float* cr = cs + (long)tp * 64 + d0;
+        const float* sr = sn + (long)tp * 64 + d0;
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          float pv = pa[e] + (bias ? bias[n + dc + e] : 0.f);
+          float rot = d0 < 32 ? -pv : pv;
+          val[e] = val[e] * cr[e] + rot * sr[e];
+        }
+      }
+      if (which == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; e++) val[e] *= 0.125f;
+      }
+      T* dst = which == 0 ? q : (which == 1 ? k : v);
+      store8<T>(dst + (((long)b * H + h) * Ntok + t) * 64 + d0, val);
+    });
+  }
+};
+
+// ------------------------------------------------------------------ fused 3 mask heads
+// per pixel: h = relu(conv3x3_64->96(feat) + b1) ; logit_k = h[32k:32k+32] . w2[k] + b2[k]
+// (src/s3od/model.py:440-452,461-467; the three Sequential heads run as one N=96 GEMM)
+template <typename T> struct EpiHeads {
+  float* logits; T* hsave; const float* b1; const float* w2; const float* b2;
+  int M, HW;
+  DEV void prepare(int) {}
+  DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN) const {
+    float* t = (float*)ct;  // relu in place
+    for (int s = tid; s < BM * 96; s += 256) {
+      int r = s / 96, c = s - r * 96;
+      t[r * LDT + c] = fmaxf(t[r * LDT + c] + b1[c], 0.f);
+    }
+    __syncthreads();
+    if (hsave) {
+      for_segments(ct, LDT, BM, 96, m0, 0, M, 96, tid, [&](int m, int n, const float* a, int, int) {
+        store8<T>(hsave + (long)m * 96 + n, a);
+      });
+    }
+    for (int s = tid; s < 3 * BM; s += 256) {
+      int k = s / BM, r = s - k * BM;
+      int m = m0 + r;
+      if (m >= M) continue;
+      const float* row = ct + r * LDT + 32 * k;
+      float acc = b2[k];
+#pragma unroll 8
+      for (int j = 0; j < 32; j++) acc += row[j] * w2[k * 32 + j];
+      int b = m / HW, pix = m - b * HW;
+      logits[((long)b * 3 + k) * HW + pix] = acc;
+    }
+  }
+};
+
+template <int BM, int BN> struct Tile {};
+
+extern "C" {
+
+// ---------------------------------------------------------------------------------- linear
+// pre = sum_k x[m,k] w[n,k] + bias[n];  out[rm(m), n] = act(pre*scale[n] + shift[n]) (+res1 +res2)
+// x: [M,K] (ld ldx) dtype T, w: [N,K] T, res: T or f32 (res_f32), out T or f32 (out_f32).
+// row_mode 0: dense; 1: token rows (m = b*P + p -> b*(P+prefix) + prefix + p)
+int s3od_linear_fwd(int dtype, int M, int N, int K, const void* x, long ldx, const void* w,
+                    const float* bias, const float* scale, const float* shift, int act,
+                    const void* res1, long ldr1, const void* res2, long ldr2, int res_f32,
+                    void* out, long ldo, int out_f32, void* pre, long ldp,
+                    int row_mode, int P, int prefix, void* stream) {
+  S3OD_REQUIRE(K % 8 == 0 && N % 8 == 0, "linear_fwd: K and N must be multiples of 8 (K=%d N=%d)", K, N);
+  RowMap rm = dense_rm(); rm.mode = row_mode; rm.P = P; rm.prefix = prefix;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    const int KTILES = cdiv(K, KT<T>::BK);
+    auto go = [&](auto tile, auto tout, auto tres) -> int {
+      typedef decltype(tout) TO; typedef decltype(tres) TR;
+      constexpr int BM = 128, BN = 128;
+      DenseKC<T, BM> la{(const T*)x, ldx, M, K, 0};
+      DenseKC<T, BN> lb{(const T*)w, (long)K, N, K, 0};
+      EpiStd<TO, TR> e{(TO*)out, ldo, 0, bias, scale, shift, (const TR*)res1, ldr1, (const TR*)res2, ldr2,
+                       (TO*)pre, ldp, nullptr, act, M, N, rm};
+      return launch_igemm<T, BM, BN>(la, lb, e, M, N, KTILES, 1, 1, st);
+    };
+    if (out_f32 && res_f32) return go(0, float{}, float{});
+    if (out_f32) return go(0, float{}, T{});
+    if (res_f32) return go(0, T{}, float{});
+    return go(0, T{}, T{});
+  });
+  return 0;
+}
+
+// dx[m, n] = sum_k dy[m,k] w[k,n]  (w: [K=out][N=in]); act=ACT_GELU_BWD multiplies by gelu'(pre)
+int s3od_linear_dgrad(int dtype, int M, int N, int K, const void* dy, long lddy, const void* w,
+                      int act, const void* aux, long ldaux, void* dx, long lddx, int out_f32, void* stream) {
+  S3OD_REQUIRE(K % 8 == 0 && N % 8 == 0, "linear_dgrad: K,N %% 8");
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    const int KTILES = cdiv(K, KT<T>::BK);
+    constexpr int BM = 128, BN = 128;
+    DenseKC<T, BM> la{(const T*)dy, lddy, M, K, 0};
+    DenseMC<T, BN> lb{(const T*)w, (long)N, K, N};
+    if (out_f32) {
+      EpiStd<float, T> e{(float*)dx, lddx, 0, nullptr, nullptr, nullptr, (const T*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, dense_rm()};
+      return launch_igemm<T, BM, BN>(la, lb, e, M, N, KTILES, 1, 1, st);
+    }
+    EpiStd<T, T> e{(T*)dx, lddx, 0, nullptr, nullptr, nullptr, (const T*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, dense_rm()};
+    return launch_igemm<T, BM, BN>(la, lb, e, M, N, KTILES, 1, 1, st);
+  });
+  return 0;
+}
+
+// dw[n_out, k_in] += sum_rows dy[row, n_out] x[row, k_in]   (fp32 atomics, split over rows)
+int s3od_linear_wgrad(int dtype, int Nout, int Kin, int rows, const void* dy, long lddy,
+                      const void* x, long ldx, float* dw, int split, void* stream) {
+  S3OD_REQUIRE(Nout % 8 == 0 && Kin % 8 == 0, "linear_wgrad: dims %% 8");
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    const int KTILES = cdiv(rows, KT<T>::BK);
+    if (split <= 0) {
+      int tiles = cdiv(Nout, 128) * cdiv(Kin, 128);
+      split = max(1, min(KTILES / 8, 2048 / max(tiles, 1)));
+    }
+    constexpr int BM = 128, BN = 128;
+    DenseMC<T, BM> la{(const T*)dy, lddy, rows, Nout};
+    DenseMC<T, BN> lb{(const T*)x, ldx, rows, Kin};
+    EpiWgrad e{dw, Nout, Kin, Kin, 1};
+    return launch_igemm<T, BM, BN>(la, lb, e, Nout, Kin, KTILES, split, 1, st);
+  });
+  return 0;
+}
+
+// fused QKV projection + bias + RoPE + head split. x: [B*Ntok, 768] T ; w: [2304, 768] T
+int s3od_qkv_rope_fwd(int dtype, int B, int Ntok, int P, const void* x, const void* w, const float* bias,
+                      const float* cos_t, const float* sin_t, void* q, void* k, void* v, void* stream) {
+  const int H = 12, D = 768, N = 3 * D, M = B * Ntok;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    constexpr int BM = 128, BN = 128;
+    DenseKC<T, BM> la{(const T*)x, (long)D, M, D, 0};
+    DenseKC<T, BN> lb{(const T*)w, (long)D, N, D, 0};
+    EpiQKV<T> e{(T*)q, (T*)k, (T*)v, bias, cos_t, sin_t, M, Ntok, P, H};
+    return launch_igemm<T, BM, BN>(la, lb, e, M, N, cdiv(D, KT<T>::BK), 1, 1, st);
+  });
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------- convs
+// NHWC activations, weights repacked [Cout][KH][KW][Cin].
+// pre = conv(relu?(x)) + bias[n]; out[b,oy,ox,n] = act(pre*scale[n] + shift[n]) (+res1 +res2);
+// stats: BN batch sums of pre.
+int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW,
+                  int stride, int pad, const void* x, int relu_in, const void* wp,
+                  const float* bias, const float* scale, const float* shift, int act, const void* res1, const void* res2,
+                  void* out, void* pre, double* stats, void* stream) {
+  S3OD_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "conv_fwd: channels %% 8 (Cin=%d Cout=%d)", Cin, Cout);
+  ConvGeo g{}; g.B = B; g.SH = H; g.SW = W; g.SC = Cin; g.RH = OH; g.RW = OW; g.KH = KH; g.KW = KW; g.s = stride; g.p = pad;
+  const int M = B * OH * OW, N = Cout, K = KH * KW * Cin;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    const int KTILES = cdiv(K, KT<T>::BK);
+    auto go = [&](auto bn) -> int {
+      constexpr int BM = 128, BN = decltype(bn)::value;
+      ConvFwdA<T, BM> la{}; la.x = (const T*)x; la.g = g; la.M = M; la.relu = relu_in;
+      DenseKC<T, BN> lb{(const T*)wp, (long)K, N, K, 0};
+      EpiStd<T, T> e{(T*)out, (long)Cout, 0, bias, scale, shift, (const T*)res1, (long)Cout, (const T*)res2, (long)Cout,
+                     (T*)pre, (long)Cout, stats, act, M, N, dense_rm()};
+      return launch_igemm<T, BM, BN>(la, lb, e, M, N, KTILES, 1, 1, st);
+    };
+    if (Cout <= 64) return go(std::integral_constant<int, 64>{});
+    return go(std::integral_constant<int, 128>{});
+  });
+  return 0;
+}
+
+// conv dgrad == ConvTranspose2d forward.  dy: [B,OH,OW,Cout] (conv output grid); w: [Cout][KH][KW][Cin];
+// dx: [B,H,W,Cin] (conv input grid).  One launch per output parity class.
+int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW,
+                    int stride, int pad, const void* dy, const void* wp,
+                    const float* bias, const float* scale, const float* shift, int act, const void* res1,
+                    void* dx, void* pre, double* stats, void* stream) {
+  S3OD_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "conv_dgrad: channels %% 8");
+  ConvGeo g0{}; g0.B = B; g0.SH = OH; g0.SW = OW; g0.SC = Cout; g0.KH = KH; g0.KW = KW; g0.s = stride; g0.p = pad;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    for (int py = 0; py < stride; py++)
+      for (int px = 0; px < stride; px++) {
+        ConvGeo g = make_class(g0, H, W, py, px);
+        const int M = B * g.RH * g.RW, N = Cin, K = g.nth * g.ntw * Cout;
+        if (M == 0) continue;
+        RowMap rm{}; rm.mode = 2; rm.RH = g.RH; rm.RW = g.RW; rm.OH = H; rm.OW = W; rm.s = stride; rm.py = py; rm.px = px;
+        auto go = [&](auto bn) -> int {
+          constexpr int BM = 128, BN = decltype(bn)::value;
+          ConvDgradA<T, BM> la{}; la.dy = (const T*)dy; la.g = g; la.M = M;
+          ConvDgradB<T, BN> lb{}; lb.w = (const T*)wp; lb.g = g; lb.NC = Cin;
+          EpiStd<T, T> e{(T*)dx, (long)Cin, 0, bias, scale, shift, (const T*)res1, (long)Cin, nullptr, 0,
+                         (T*)pre, (long)Cin, stats, act, M, N, rm};
+          return launch_igemm<T, BM, BN>(la, lb, e, M, N, cdiv(K, KT<T>::BK), 1, 1, st);
+        };
+        int rc = Cin <= 64 ? go(std::integral_constant<int, 64>{}) : go(std::integral_constant<int, 128>{});
+        if (rc) return rc;
+      }
+  });
+  return 0;
+}
+
+// conv wgrad: dw[Cout][Cin][KH][KW] (PyTorch layout, fp32) += sum_pix dy[pix][co] * x[src(pix,tap)][ci]
+// dy: [B,OH,OW,Cout]; x: [B,H,W,Cin].  Also serves ConvTranspose2d weights (conv view).
+int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW,
+                    int stride, int pad, const void* dy, const void* x, float* dw, int split, void* stream) {
+  S3OD_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "conv_wgrad: channels %% 8");
+  ConvGeo g{}; g.B = B; g.SH = H; g.SW = W; g.SC = Cin; g.RH = OH; g.RW = OW; g.KH = KH; g.KW = KW; g.s = stride; g.p = pad;
+  const int NPIX = B * OH * OW, M = Cout, N = KH * KW * Cin;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    const int KTILES = cdiv(NPIX, KT<T>::BK);
+    auto go = [&](auto bm) -> int {
+      constexpr int BM = decltype(bm)::value, BN = 128;
+      int sp = split;
+      if (sp <= 0) { int tiles = cdiv(M, BM) * cdiv(N, BN); sp = max(1, min(KTILES / 8, 2048 / max(tiles, 1))); }
+      DenseMC<T, BM> la{(const T*)dy, (long)Cout, NPIX, Cout};
+      WgradB<T, BN> lb{}; lb.x = (const T*)x; lb.g = g; lb.NPIX = NPIX;
+      EpiWgrad e{dw, M, N, Cin, KH * KW};
+      return launch_igemm<T, BM, BN>(la, lb, e, M, N, KTILES, sp, 1, st);
+    };
+    if (Cout <= 64) return go(std::integral_constant<int, 64>{});
+    return go(std::integral_constant<int, 128>{});
+  });
+  return 0;
+}
+
+// three 3x3 64->32 + ReLU + 1x1 32->1 mask heads as one GEMM (N=96) with a fused epilogue.
+// feat: [B,H,W,64] T ; w1p: [96][3][3][64] T ; b1: [96]; w2: [3][32]; b2: [3]
+// logits: [B,3,H,W] fp32 (NCHW, the reference output layout); hsave: optional [B*H*W, 96] T
+int s3od_mask_heads_fwd(int dtype, int B, int H, int W, const void* feat, const void* w1p, const float* b1,
+                        const float* w2, const float* b2, float* logits, void* hsave, void* stream) {
+  ConvGeo g{}; g.B = B; g.SH = H; g.SW = W; g.SC = 64; g.RH = H; g.RW = W; g.KH = 3; g.KW = 3; g.s = 1; g.p = 1;
+  const int M = B * H * W, N = 96, K = 9 * 64;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    constexpr int BM = 128, BN = 128;
+    ConvFwdA<T, BM> la{}; la.x = (const T*)feat; la.g = g; la.M = M; la.relu = 0;
+    DenseKC<T, BN> lb{(const T*)w1p, (long)K, N, K, 0};
+    EpiHeads<T> e{logits, (T*)hsave, b1, w2, b2, M, H * W};
+    return launch_igemm<T, BM, BN>(la, lb, e, M, BN, cdiv(K, KT<T>::BK), 1, 1, st);
+  });
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,326 @@
+// Memory-bound ViT kernels: patch im2col, token prefix, RoPE table, LayerNorm fwd/bwd,
+// tap cast, bias / LayerScale gradient reductions, QKV-gradient RoPE inverse.
+// DINOv3 arithmetic follows tf:models/dinov3_vit/modeling_dinov3_vit.py (transformers).
+#include "common.hpp"
+
+#define DISPATCH_T(dtype, ...)                                                  \
+  do {                                                                          \
+    if ((dtype) == S3OD_BF16) { typedef bf16 T; __VA_ARGS__ }                   \
+    else if ((dtype) == S3OD_F32) { typedef float T; __VA_ARGS__ }              \
+    else { s3od_set_error("bad dtype %d", (int)(dtype)); return 22; }           \
+  } while (0)
+
+// ---------------------------------------------------------------- patch embed im2col
+// x: [B,3,H,W] f32 NCHW -> cols [B*P, 768] T, k = c*256 + kh*16 + kw (conv weight flatten order)
+template <typename T>
+__global__ void patch_im2col_kernel(const float* __restrict__ x, T* __restrict__ cols, int B, int H, int W) {
+  const int ph = H / 16, pw = W / 16, P = ph * pw;
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;   // one (b, p, c, kh) row of 16 pixels
+  long total = (long)B * P * 48;
+  if (idx >= total) return;
+  int ckh = idx % 48; long bp = idx / 48;
+  int p = bp % P; int b = bp / P;
+  int c = ckh / 16, kh = ckh % 16;
+  int py = p / pw, px = p % pw;
+  const float* src = x + (((long)b * 3 + c) * H + py * 16 + kh) * W + px * 16;
+  T* dst = cols + bp * 768 + c * 256 + kh * 16;
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 4; i++) { float4 f = ((const float4*)src)[i]; v[4 * i] = f.x; v[4 * i + 1] = f.y; v[4 * i + 2] = f.z; v[4 * i + 3] = f.w; }
+  store8<T>(dst, v);
+  store8<T>(dst + 8, v + 8);
+}
+
+// rows 0..4 of each image: cls + 4 register tokens (tf:…:88-90)
+__global__ void token_prefix_kernel(float* x, const float* cls, const float* reg, int Ntok) {
+  int b = blockIdx.x, t = blockIdx.y;  // t in 0..4
+  const float* src = t == 0 ? cls : reg + (t - 1) * 768;
+  float* dst = x + ((long)b * Ntok + t) * 768;
+  for (int i = threadIdx.x; i < 768; i += blockDim.x) dst[i] = src[i];
+}
+
+// RoPE table (tf:…:96-121, 168-200): cos/sin [P,64]; rescale <= 0 means none (eval)
+__global__ void rope_table_kernel(float* cs, float* sn, int ph, int pw, float rescale) {
+  int p = blockIdx.x, j = threadIdx.x;  // 64 threads
+  if (p >= ph * pw) return;
+  int jj = j & 31;
+  int f = jj & 15;
+  // inv_freq = 1 / 100 ** arange(0, 1, 4/64)
+  float expo = (float)f * (4.0f / 64.0f);
+  float inv_freq = 1.0f / powf(100.0f, expo);
+  int y = p / pw, xq = p % pw;
+  float coord = jj < 16 ? ((float)y + 0.5f) / (float)ph : ((float)xq + 0.5f) / (float)pw;
+  coord = 2.0f * coord - 1.0f;
+  if (rescale > 0.f) coord = coord * rescale;
+  float ang = (6.283185307179586f * coord) * inv_freq;
+  cs[p * 64 + j] = cosf(ang);
+  sn[p * 64 + j] = sinf(ang);
+}
+
+// ---------------------------------------------------------------- LayerNorm (D = 768)
+// one wave per row; fp32 statistics; y = (x-mean)*rstd*w + b  stored as T
+template <typename T>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                      const float* __restrict__ b, T* __restrict__ y,
+                                                      float* __restrict__ mean_o, float* __restrict__ rstd_o, int M, float eps) {
+  int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* xr = x + (long)row * 768;
+  float v[12];
+#pragma unroll
+  for (int i = 0; i < 3; i++) { float4 f = ((const float4*)xr)[lane + 64 * i]; v[4 * i] = f.x; v[4 * i + 1] = f.y; v[4 * i + 2] = f.z; v[4 * i + 3] = f.w; }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 12; i++) s += v[i];
+  float mean = warp_sum(s) * (1.0f / 768.0f);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 12; i++) { float d = v[i] - mean; q += d * d; }
+  float var = warp_sum(q) * (1.0f / 768.0f);
+  float rstd = 1.0f / sqrtf(var + eps);
+  T* yr = y + (long)row * 768;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    int c = 4 * (lane + 64 * i);
+    float4 wf = *(const float4*)(w + c), bf = *(const float4*)(b + c);
+    float o0 = (v[4 * i] - mean) * rstd * wf.x + bf.x, o1 = (v[4 * i + 1] - mean) * rstd * wf.y + bf.y;
+    float o2 = (v[4 * i + 2] - mean) * rstd * wf.z + bf.z, o3 = (v[4 * i + 3] - mean) * rstd * wf.w + bf.w;
+    if constexpr (sizeof(T) == 4) *(float4*)(yr + c) = make_float4(o0, o1, o2, o3);
+    else { bf16x4 o = {(bf16)o0, (bf16)o1, (bf16)o2, (bf16)o3}; *(bf16x4*)(yr + c) = o; }
+  }
+  if (lane == 0) { mean_o[row] = mean; rstd_o[row] = rstd; }
+}
+
+// LayerNorm backward. dx = dres + rstd*(g - mean(g) - xhat*mean(g*xhat)), g = dy*w
+// dw += sum dy*xhat ; db += sum dy   (fp32 block partials -> atomics)
+template <typename T>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, const float* __restrict__ x,
+                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                      const float* __restrict__ w, const float* __restrict__ dres,
+                                                      float* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db,
+                                                      int M, int rows_per_block) {
+  __shared__ float sdw[768], sdb[768];
+  for (int i = threadIdx.x; i < 768; i += 256) { sdw[i] = 0.f; sdb[i] = 0.f; }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float pw[12], pb[12];
+#pragma unroll
+  for (int i = 0; i < 12; i++) { pw[i] = 0.f; pb[i] = 0.f; }
+  int r0 = blockIdx.x * rows_per_block;
+  for (int row = r0 + wave; row < min(M, r0 + rows_per_block); row += 4) {
+    const float* xr = x + (long)row * 768;
+    float mu = mean[row], rs = rstd[row];
+    float xh[12], g[12], dyv[12];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      int c = 4 * (lane + 64 * i);
+      float4 xf = *(const float4*)(xr + c);
+      float4 wf = *(const float4*)(w + c);
+      float d4[4];
+      if constexpr (sizeof(T) == 4) { float4 t = *(const float4*)(dy + (long)row * 768 + c); d4[0] = t.x; d4[1] = t.y; d4[2] = t.z; d4[3] = t.w; }
+      else { bf16x4 t = *(const bf16x4*)(dy + (long)row * 768 + c); d4[0] = (float)t[0]; d4[1] = (float)t[1]; d4[2] = (float)t[2]; d4[3] = (float)t[3]; }
+      float xs[4] = {xf.x, xf.y, xf.z, xf.w}, ws[4] = {wf.x, wf.y, wf.z, wf.w};
+#pragma unroll
+      for (int e = 0; e < 4; e++) { xh[4 * i + e] = (xs[e] - mu) * rs; dyv[4 * i + e] = d4[e]; g[4 * i + e] = d4[e] * ws[e]; }
+    }
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 12; i++) { s1 += g[i]; s2 += g[i] * xh[i]; }
+    s1 = warp_sum(s1) * (1.0f / 768.0f);
+    s2 = warp_sum(s2) * (1.0f / 768.0f);
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      int c = 4 * (lane + 64 * i);
+      float o[4];
+      float4 r = dres ? *(const float4*)(dres + (long)row * 768 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float rr[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        int k = 4 * i + e;
+        o[e] = rr[e] + rs * (g[k] - s1 - xh[k] * s2);
+        pw[k] += dyv[k] * xh[k];
+        pb[k] += dyv[k];
+      }
+      *(float4*)(dx + (long)row * 768 + c) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      int c = 4 * (lane + 64 * i) + e;
+      atomicAdd(&sdw[c], pw[4 * i + e]);
+      atomicAdd(&sdb[c], pb[4 * i + e]);
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 768; i += 256) { atomicAdd(dw + i, sdw[i]); atomicAdd(db + i, sdb[i]); }
+}
+
+// taps: x f32 [B, Ntok, 768] -> T [B, P, 768] (drop 1 + 4 prefix tokens; src/s3od/model.py:75-84)
+template <typename T>
+__global__ void cast_tap_kernel(const float* __restrict__ x, T* __restrict__ y, int B, int Ntok, int P) {
+  long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  long total = (long)B * P * 768;
+  if (i >= total) return;
+  long row = i / 768; int c = i % 768;
+  int b = row / P, p = row % P;
+  float v[8];
+  load8<float>(x + ((long)b * Ntok + (Ntok - P) + p) * 768 + c, v);
+  store8<T>(y + i, v);
+}
+
+// column sums of a [M, N] T matrix (bias gradients): out[n] += sum_m a[m, n]
+template <typename T>
+__global__ void colsum_kernel(const T* __restrict__ a, long lda, int M, int N, float* __restrict__ out, int rows_per_block) {
+  int n = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (n >= N) return;
+  int r0 = blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int r = r0; r < r1; r++) {
+    float v[8]; load8<T>(a + (long)r * lda + n, v);
+#pragma unroll
+    for (int e = 0; e < 8; e++) s[e] += v[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 8; e++) atomicAdd(out + n + e, s[e]);
+}
+
+// LayerScale backward: du = dx * lam (T); dlam[n] += sum_m dx*u ; dbias[n] += sum_m du
+template <typename T>
+__global__ void scale_bwd_kernel(const float* __restrict__ dx, const T* __restrict__ u, const float* __restrict__ lam,
+                                 T* __restrict__ du, float* __restrict__ dlam, float* __restrict__ dbias, int M, int rows_per_block) {
+  int n = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (n >= 768) return;
+  int r0 = blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  float l[8]; load8<float>(lam + n, l);
+  float sl[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int r = r0; r < r1; r++) {
+    float d[8], uu[8], o[8];
+    load8<float>(dx + (long)r * 768 + n, d);
+    load8<T>(u + (long)r * 768 + n, uu);
+#pragma unroll
+    for (int e = 0; e < 8; e++) { o[e] = d[e] * l[e]; sl[e] += d[e] * uu[e]; sb[e] += o[e]; }
+    store8<T>(du + (long)r * 768 + n, o);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; e++) { atomicAdd(dlam + n + e, sl[e]); atomicAdd(dbias + n + e, sb[e]); }
+}
+
+// dq,dk,dv [B,H,N,64] (dq w.r.t. the 1/8-scaled, rotated q) -> dqkv [B*N, 2304] T w.r.t. the
+// pre-RoPE projections: d(pre) = cos*dy - R(sin*dy), R = rotate_half; dq additionally * 1/8.
+template <typename T>
+__global__ void qkv_unrope_kernel(const T* __restrict__ dq, const T* __restrict__ dk, const T* __restrict__ dv,
+                                  const float* __restrict__ cs, const float* __restrict__ sn,
+                                  T* __restrict__ dqkv, int B, int Ntok, int P) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;   // (m, which, h, d8)
+  long total = (long)B * Ntok * 3 * 12 * 8;
+  if (idx >= total) return;
+  int d8 = idx % 8; long r = idx / 8;
+  int h = r % 12; r /= 12;
+  int which = r % 3; long m = r / 3;
+  int b = m / Ntok, t = m % Ntok;
+  const T* src = which == 0 ? dq : (which == 1 ? dk : dv);
+  const T* row = src + (((long)b * 12 + h) * Ntok + t) * 64;
+  int d0 = d8 * 8;
+  float v[8];
+  load8<T>(row + d0, v);
+  if (which < 2 && t >= Ntok - P) {
+    int tp = t - (Ntok - P);
+    int pd = d0 < 32 ? d0 + 32 : d0 - 32;
+    float pv[8]; load8<T>(row + pd, pv);
+    const float* cr = cs + (long)tp * 64; const float* sr = sn + (long)tp * 64;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      int d = d0 + e, dp = pd + e;
+      // y = x*cos + R(x)*sin  =>  dx = cos*dy + R^T(sin*dy);  R^T(z)[d] = z[d+32] (d<32), -z[d-32] (d>=32)
+      float rt = d < 32 ? sr[dp] * pv[e] : -sr[dp] * pv[e];
+      o[e] = cr[d] * v[e] + rt;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; e++) v[e] = o[e];
+  }
+  if (which == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; e++) v[e] *= 0.125f;
+  }
+  store8<T>(dqkv + m * 2304 + which * 768 + h * 64 + d0, v);
+}
+
+extern "C" {
+
+int s3od_patch_im2col(int dtype, const float* x, void* cols, int B, int H, int W, void* stream) {
+  S3OD_REQUIRE(W % 4 == 0 && H >= 16 && W >= 16, "patch_im2col: W must be a multiple of 4 and H,W >= 16");
+  long total = (long)B * (H / 16) * (W / 16) * 48;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL(patch_im2col_kernel<T>, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream, x, (T*)cols, B, H, W);
+  });
+  return s3od_check_launch("patch_im2col");
+}
+
+int s3od_token_prefix(float* x, const float* cls, const float* reg, int B, int Ntok, void* stream) {
+  hipLaunchKernelGGL(token_prefix_kernel, dim3(B, 5), dim3(256), 0, (hipStream_t)stream, x, cls, reg, Ntok);
+  return s3od_check_launch("token_prefix");
+}
+
+int s3od_rope_table(float* cs, float* sn, int ph, int pw, float rescale, void* stream) {
+  hipLaunchKernelGGL(rope_table_kernel, dim3(ph * pw), dim3(64), 0, (hipStream_t)stream, cs, sn, ph, pw, rescale);
+  return s3od_check_launch("rope_table");
+}
+
+int s3od_layernorm_fwd(int dtype, const float* x, const float* w, const float* b, void* y, float* mean, float* rstd,
+                       int M, float eps, void* stream) {
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL(ln_fwd_kernel<T>, dim3(cdiv(M, 4)), dim3(256), 0, (hipStream_t)stream, x, w, b, (T*)y, mean, rstd, M, eps);
+  });
+  return s3od_check_launch("layernorm_fwd");
+}
+
+int s3od_layernorm_bwd(int dtype, const void* dy, const float* x, const float* mean, const float* rstd, const float* w,
+                       const float* dres, float* dx, float* dw, float* db, int M, void* stream) {
+  const int rpb = 64;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3(cdiv(M, rpb)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, x, mean, rstd, w, dres, dx, dw, db, M, rpb);
+  });
+  return s3od_check_launch("layernorm_bwd");
+}
+
+int s3od_cast_tap(int dtype, const float* x, void* y, int B, int Ntok, int P, void* stream) {
+  long total = (long)B * P * 768 / 8;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL(cast_tap_kernel<T>, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream, x, (T*)y, B, Ntok, P);
+  });
+  return s3od_check_launch("cast_tap");
+}
+
+int s3od_colsum(int dtype, const void* a, long lda, int M, int N, float* out, void* stream) {
+  S3OD_REQUIRE(N % 8 == 0, "colsum: N %% 8");
+  const int rpb = 256;
+  dim3 grid(cdiv(N / 8, 256), cdiv(M, rpb));
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL(colsum_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)a, lda, M, N, out, rpb);
+  });
+  return s3od_check_launch("colsum");
+}
+
+int s3od_layerscale_bwd(int dtype, const float* dx, const void* u, const float* lam, void* du, float* dlam, float* dbias,
+                        int M, void* stream) {
+  const int rpb = 128;
+  dim3 grid(1, cdiv(M, rpb));
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL(scale_bwd_kernel<T>, grid, dim3(96), 0, (hipStream_t)stream, dx, (const T*)u, lam, (T*)du, dlam, dbias, M, rpb);
+  });
+  return s3od_check_launch("layerscale_bwd");
+}
+
+int s3od_qkv_unrope(int dtype, const void* dq, const void* dk, const void* dv, const float* cs, const float* sn,
+                    void* dqkv, int B, int Ntok, int P, void* stream) {
+  long total = (long)B * Ntok * 3 * 12 * 8;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL(qkv_unrope_kernel<T>, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const T*)dq, (const T*)dk, (const T*)dv, cs, sn, (T*)dqkv, B, Ntok, P);
+  });
+  return s3od_check_launch("qkv_unrope");
+}
+
+}  // extern "C"

@@ -1,0 +1,338 @@
+"""Native executor of the S3OD hot path: DINOv3 ViT-B/16 encoder + DPT decoder + mask heads.
+
+Every arithmetic op runs in libs3od_hip.so (gfx950 HIP kernels); PyTorch only provides
+device memory (caching allocator), streams and the autograd / nn.Module surface.
+
+Layouts: tokens [B, Ntok, 768] (fp32 residual stream); q/k/v [B*12, Ntok, 64]; decoder
+activations NHWC [B, H, W, C]; compute dtype T = bf16 (fast) or f32 (strict parity).
+Parameters stay fp32 in the reference's state_dict layout; ``prepare()`` repacks them into
+kernel layouts ([Cout][KH][KW][Cin], fused QKV [2304][768]) in T.
+
+Reference structure: src/s3od/model.py:62-467 and tf:models/dinov3_vit/modeling_dinov3_vit.py.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+from ._lib import lib, stream, F32, BF16
+from .weights import N_LAYERS, TAPS, OUT_CH
+
+H_, D_, NREG = 12, 768, 4
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_GELU_BWD, ACT_RELU_BWD = 0, 1, 2, 3, 4
+LAST_LAYER = max(TAPS)          # layers >= 11 (and the final norm) never reach the outputs
+
+
+def _E(ref, n, dt, dev):
+    return torch.empty(n, dtype=dt, device=dev)
+
+
+@dataclass
+class Ctx:
+    """Tensors saved by a training forward for the native backward."""
+    B: int = 0
+    H: int = 0
+    W: int = 0
+    ph: int = 0
+    pw: int = 0
+    t: dict = field(default_factory=dict)
+
+
+class DPTEngine:
+    def __init__(self, params: dict, buffers: dict, compute_dtype: str = "bf16"):
+        """params / buffers: name -> fp32 CUDA tensor in the reference layout (canonical keys)."""
+        self.p = params
+        self.buf = buffers
+        self.set_dtype(compute_dtype)
+        self.w = {}
+        self._wkey = None
+
+    def set_dtype(self, compute_dtype):
+        assert compute_dtype in ("bf16", "f32")
+        self.cdt = compute_dtype
+        self.dt = BF16 if compute_dtype == "bf16" else F32
+        self.tdt = torch.bfloat16 if compute_dtype == "bf16" else torch.float32
+        self._wkey = None
+
+    # ------------------------------------------------------------------ weights
+    def _version_key(self):
+        return (self.cdt, sum(int(v._version) for v in self.p.values()), id(self))
+
+    def prepare(self, force=False):
+        """Repack / cast all fp32 parameters into kernel layouts (cached until params change)."""
+        key = self._version_key()
+        if not force and key == self._wkey:
+            return
+        L, P, dt, T = lib(), self.p, self.dt, self.tdt
+        st = stream()
+        dev = next(iter(P.values())).device
+        w = {}
+
+        def pack(name, O, I, KH=1, KW=1, out=None):
+            out = torch.empty((O, KH, KW, I), dtype=T, device=dev) if out is None else out
+            L("s3od_repack_weight", dt, P[name], out, O, I, KH, KW, st)
+            return out
+
+        e = "encoder.embeddings."
+        w["pe"] = pack(e + "patch_embeddings.weight", D_, 3 * 16 * 16)
+        for i in range(LAST_LAYER):
+            p = f"encoder.model.layer.{i}."
+            qkv = torch.empty((3 * D_, D_), dtype=T, device=dev)
+            pack(p + "attention.q_proj.weight", D_, D_, out=qkv[0:D_])
+            pack(p + "attention.k_proj.weight", D_, D_, out=qkv[D_:2 * D_])
+            pack(p + "attention.v_proj.weight", D_, D_, out=qkv[2 * D_:])
+            w[f"qkv{i}"] = qkv
+            bq = torch.zeros(3 * D_, dtype=torch.float32, device=dev)
+            bq[:D_].copy_(P[p + "attention.q_proj.bias"])
+            bq[2 * D_:].copy_(P[p + "attention.v_proj.bias"])
+            w[f"bqkv{i}"] = bq
+            w[f"o{i}"] = pack(p + "attention.o_proj.weight", D_, D_)
+            w[f"up{i}"] = pack(p + "mlp.up_proj.weight", 3072, D_)
+            w[f"down{i}"] = pack(p + "mlp.down_proj.weight", D_, 3072)
+        h = "seg_head."
+        for i, c in enumerate(OUT_CH):
+            w[f"proj{i}"] = pack(h + f"projects.{i}.weight", c, D_)
+        w["rs0"] = pack(h + "resize_layers.0.weight", 256, 256, 4, 4)   # ConvT: [Cin_T][Cout_T] = conv view
+        w["rs1"] = pack(h + "resize_layers.1.weight", 512, 512, 2, 2)
+        w["rs3"] = pack(h + "resize_layers.3.weight", 1024, 1024, 3, 3)
+        for i, c in enumerate(OUT_CH):
+            w[f"rn{i + 1}"] = pack(h + f"scratch.layer{i + 1}_rn.weight", 256, c, 3, 3)
+        for r in (1, 2, 3, 4):
+            q = h + f"scratch.refinenet{r}."
+            w[f"ref{r}.out"] = pack(q + "out_conv.weight", 256, 256)
+            for u in (1, 2):
+                for cv in (1, 2):
+                    w[f"ref{r}.u{u}.c{cv}"] = pack(q + f"resConfUnit{u}.conv{cv}.weight", 256, 256, 3, 3)
+        m = h + "mask_head."
+        w["oc1"] = pack(m + "output_conv1.weight", 128, 256, 3, 3)
+        w["up2x"] = pack(m + "upsample_2x.0.weight", 128, 64, 4, 4)     # ConvT [128][64][4][4]
+        w["c64"] = pack(m + "upsample_2x.2.weight", 64, 64, 3, 3)
+        heads = torch.empty((96, 3, 3, 64), dtype=T, device=dev)
+        for k in range(3):
+            pack(m + f"mask_heads.{k}.0.weight", 32, 64, 3, 3, out=heads[32 * k:32 * (k + 1)])
+        w["heads1"] = heads
+        w["heads1_b"] = torch.cat([P[m + f"mask_heads.{k}.0.bias"] for k in range(3)])
+        w["heads2"] = torch.cat([P[m + f"mask_heads.{k}.2.weight"].reshape(32) for k in range(3)])
+        w["heads2_b"] = torch.cat([P[m + f"mask_heads.{k}.2.bias"] for k in range(3)])
+        self.w = w
+        self._wkey = key
+
+    # ------------------------------------------------------------------ helpers
+    def _lin(self, x, w, M, N, K, out, bias=None, scale=None, shift=None, act=ACT_NONE, res1=None, res_f32=False,
+             out_f32=False, pre=None, row_mode=0, P=0, prefix=0, ldx=None, ldo=None, ldr=None):
+        lib()("s3od_linear_fwd", self.dt, M, N, K, x, ldx or K, w, bias, scale, shift, act,
+              res1, ldr or N, None, 0, int(res_f32), out, ldo or N, int(out_f32), pre, N,
+              row_mode, P, prefix, stream())
+
+    def _conv(self, x, w, B, H, W, Cin, Cout, k, s, p, bias=None, scale=None, shift=None, act=ACT_NONE,
+              relu_in=False, res1=None, res2=None, out=None, pre=None, stats=None):
+        OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        if out is None:
+            out = torch.empty((B, OH, OW, Cout), dtype=self.tdt, device=x.device)
+        lib()("s3od_conv_fwd", self.dt, B, H, W, Cin, OH, OW, Cout, k, k, s, p, x, int(relu_in), w,
+              bias, scale, shift, act, res1, res2, out, pre, stats, stream())
+        return out
+
+    def _convT(self, x, w, B, IH, IW, Cin_T, Cout_T, k, s, p, bias=None, act=ACT_NONE, out=None):
+        """ConvTranspose2d forward == conv dgrad with the conv-view weight (no flip)."""
+        OH, OW = (IH - 1) * s - 2 * p + k, (IW - 1) * s - 2 * p + k
+        if out is None:
+            out = torch.empty((B, OH, OW, Cout_T), dtype=self.tdt, device=x.device)
+        lib()("s3od_conv_dgrad", self.dt, B, OH, OW, Cout_T, IH, IW, Cin_T, k, k, s, p, x, w,
+              bias, None, None, act, None, out, None, None, stream())
+        return out
+
+    def _bilinear(self, x, B, IH, IW, OH, OW, C):
+        y = torch.empty((B, OH, OW, C), dtype=self.tdt, device=x.device)
+        lib()("s3od_bilinear_fwd", self.dt, x, y, B, IH, IW, OH, OW, C, stream())
+        return y
+
+    # ------------------------------------------------------------------ encoder
+    def encoder_forward(self, x, train=False, rope_rescale=None, ctx=None):
+        L, P, W8, dt, T = lib(), self.p, self.w, self.dt, self.tdt
+        st = stream()
+        B, _, Hh, Ww = x.shape
+        ph, pw = Hh // 16, Ww // 16
+        NP = ph * pw
+        Nt = NP + 1 + NREG
+        M = B * Nt
+        dev = x.device
+        cs = _E(None, (NP, 64), torch.float32, dev)
+        sn = _E(None, (NP, 64), torch.float32, dev)
+        L("s3od_rope_table", cs, sn, ph, pw, float(rope_rescale) if (train and rope_rescale) else -1.0, st)
+        cols = _E(None, (B * NP, D_), T, dev)
+        L("s3od_patch_im2col", dt, x, cols, B, Hh, Ww, st)
+        xs = _E(None, (B, Nt, D_), torch.float32, dev)
+        e = "encoder.embeddings."
+        self._lin(cols, W8["pe"], B * NP, D_, D_, xs, bias=P[e + "patch_embeddings.bias"], out_f32=True,
+                  row_mode=1, P=NP, prefix=1 + NREG)
+        L("s3od_token_prefix", xs, P[e + "cls_token"], P[e + "register_tokens"], B, Nt, st)
+        if ctx is not None:
+            ctx.t.update(cols=cols, cos=cs, sin=sn)
+        taps = []
+        h1 = _E(None, (M, D_), T, dev)
+        q = _E(None, (B * H_, Nt, 64), T, dev)
+        k = torch.empty_like(q)
+        v = torch.empty_like(q)
+        o = _E(None, (M, D_), T, dev)
+        a = _E(None, (M, 3072), T, dev)
+        for i in range(LAST_LAYER):
+            p = f"encoder.model.layer.{i}."
+            if ctx is not None:   # fresh buffers per layer for the backward
+                h1 = _E(None, (M, D_), T, dev); q = _E(None, (B * H_, Nt, 64), T, dev)
+                k = torch.empty_like(q); v = torch.empty_like(q); o = _E(None, (M, D_), T, dev)
+                a = _E(None, (M, 3072), T, dev)
+                mean1 = _E(None, (M,), torch.float32, dev); rstd1 = torch.empty_like(mean1)
+                mean2 = torch.empty_like(mean1); rstd2 = torch.empty_like(mean1)
+                lse = _E(None, (B * H_, Nt), torch.float32, dev)
+                u1 = _E(None, (M, D_), T, dev); u2 = _E(None, (M, D_), T, dev)
+                hpre = _E(None, (M, 3072), T, dev); h2 = _E(None, (M, D_), T, dev)
+            else:
+                mean1 = rstd1 = mean2 = rstd2 = _E(None, (M,), torch.float32, dev)
+                lse = None; u1 = u2 = hpre = None
+                h2 = h1
+            L("s3od_layernorm_fwd", dt, xs, P[p + "norm1.weight"], P[p + "norm1.bias"], h1, mean1, rstd1, M, 1e-5, st)
+            L("s3od_qkv_rope_fwd", dt, B, Nt, NP, h1, W8[f"qkv{i}"], W8[f"bqkv{i}"], cs, sn, q, k, v, st)
+            L("s3od_attn_fwd", dt, q, k, v, o, lse, B, H_, Nt, st)
+            xm = _E(None, (B, Nt, D_), torch.float32, dev)
+            self._lin(o, W8[f"o{i}"], M, D_, D_, xm, bias=P[p + "attention.o_proj.bias"],
+                      scale=P[p + "layer_scale1.lambda1"], res1=xs, res_f32=True, out_f32=True, pre=u1)
+            L("s3od_layernorm_fwd", dt, xm, P[p + "norm2.weight"], P[p + "norm2.bias"], h2, mean2, rstd2, M, 1e-5, st)
+            self._lin(h2, W8[f"up{i}"], M, 3072, D_, a, bias=P[p + "mlp.up_proj.bias"], act=ACT_GELU, pre=hpre)
+            xn = _E(None, (B, Nt, D_), torch.float32, dev)
+            self._lin(a, W8[f"down{i}"], M, D_, 3072, xn, bias=P[p + "mlp.down_proj.bias"],
+                      scale=P[p + "layer_scale2.lambda1"], res1=xm, res_f32=True, out_f32=True, pre=u2)
+            if ctx is not None:
+                ctx.t[f"L{i}"] = dict(x=xs, h1=h1, mean1=mean1, rstd1=rstd1, q=q, k=k, v=v, o=o, lse=lse, u1=u1,
+                                      xm=xm, h2=h2, mean2=mean2, rstd2=rstd2, hpre=hpre, a=a, u2=u2)
+            xs = xn
+            if i + 1 in TAPS:
+                tp = _E(None, (B, NP, D_), T, dev)
+                L("s3od_cast_tap", dt, xs, tp, B, Nt, NP, st)
+                taps.append(tp)
+        return taps, (B, ph, pw, Nt)
+
+    # ------------------------------------------------------------------ decoder
+    def _rcu(self, x, r, u, B, h, w, train, ctx, x0=None):
+        """ResidualConvUnit (src/s3od/model.py:334-345) [+ x0 for the fusion add]."""
+        P, W8 = self.p, self.w
+        q = f"seg_head.scratch.refinenet{r}.resConfUnit{u}."
+        tag = f"ref{r}.u{u}"
+        if not train:
+            st = stream()
+            s1, t1 = self._bnfold(q + "bn1", st)
+            s2, t2 = self._bnfold(q + "bn2", st)
+            a1 = self._conv(x, W8[tag + ".c1"], B, h, w, 256, 256, 3, 1, 1, bias=P[q + "conv1.bias"], scale=s1, shift=t1,
+                            act=ACT_RELU, relu_in=True)
+            return self._conv(a1, W8[tag + ".c2"], B, h, w, 256, 256, 3, 1, 1, bias=P[q + "conv2.bias"], scale=s2,
+                              shift=t2, res1=x, res2=x0)
+        L, st, dev = lib(), stream(), x.device
+        npix = B * h * w
+        z1 = self._conv_bn_train(x, W8[tag + ".c1"], B, h, w, P[q + "conv1.bias"], relu_in=True)
+        bn1 = self._bn_train(z1["stats"], npix, q + "bn1")
+        a1 = torch.empty_like(z1["z"])
+        L("s3od_affine_act", self.dt, z1["z"], bn1["scale"], bn1["shift"], 1, None, None, a1, a1.numel(), 256, st)
+        z2 = self._conv_bn_train(a1, W8[tag + ".c2"], B, h, w, P[q + "conv2.bias"])
+        bn2 = self._bn_train(z2["stats"], npix, q + "bn2")
+        out = torch.empty_like(z2["z"])
+        L("s3od_affine_act", self.dt, z2["z"], bn2["scale"], bn2["shift"], 0, x, x0, out, out.numel(), 256, st)
+        ctx.t[tag] = dict(x=x, z1=z1["z"], a1=a1, z2=z2["z"], bn1=bn1, bn2=bn2, h=h, w=w)
+        return out
+
+    def _conv_bn_train(self, x, wt, B, h, w, bias, relu_in=False):
+        stats = torch.zeros(2 * 256, dtype=torch.float64, device=x.device)
+        z = self._conv(x, wt, B, h, w, 256, 256, 3, 1, 1, bias=bias, relu_in=relu_in, stats=stats)
+        return dict(z=z, stats=stats)
+
+    def _bn_train(self, stats, npix, name):
+        P, dev = self.p, stats.device
+        d = {k: torch.empty(256, dtype=torch.float32, device=dev) for k in ("mean", "rstd", "scale", "shift")}
+        lib()("s3od_bn_finalize", stats, npix, P[name + ".weight"], P[name + ".bias"], self.buf[name + ".running_mean"],
+              self.buf[name + ".running_var"], 0.1, 1e-5, d["mean"], d["rstd"], d["scale"], d["shift"], 256, stream())
+        nbt = self.buf.get(name + ".num_batches_tracked")
+        if nbt is not None:
+            nbt.add_(1)
+        return d
+
+    def _bnfold(self, name, st):
+        P = self.p
+        s = torch.empty(256, dtype=torch.float32, device=P[name + ".weight"].device)
+        t = torch.empty_like(s)
+        lib()("s3od_bn_fold", P[name + ".weight"], P[name + ".bias"], self.buf[name + ".running_mean"],
+              self.buf[name + ".running_var"], 1e-5, s, t, 256, st)
+        return s, t
+
+    def _fusion(self, r, x0, x1, B, h, w, oh, ow, train, ctx):
+        """FeatureFusionBlock (src/s3od/model.py:383-405). out_conv (1x1, bias) runs before the
+        bilinear resize: both are linear and bilinear weights sum to one, so the order commutes."""
+        P, W8 = self.p, self.w
+        s = x0 if x1 is None else self._rcu(x1, r, 1, B, h, w, train, ctx, x0=x0)
+        s = self._rcu(s, r, 2, B, h, w, train, ctx)
+        q = f"seg_head.scratch.refinenet{r}."
+        c = torch.empty_like(s)
+        self._lin(s, W8[f"ref{r}.out"], B * h * w, 256, 256, c, bias=P[q + "out_conv.bias"])
+        if ctx is not None:
+            ctx.t[f"ref{r}"] = dict(s=s, h=h, w=w, oh=oh, ow=ow)
+        return self._bilinear(c, B, h, w, oh, ow, 256)
+
+    def decoder_forward(self, taps, B, ph, pw, train=False, ctx=None):
+        L, P, W8, dt = lib(), self.p, self.w, self.dt
+        st = stream()
+        h = "seg_head."
+        dev = taps[0].device
+        NP = ph * pw
+        proj = []
+        for i, c in enumerate(OUT_CH):
+            y = torch.empty((B, ph, pw, c), dtype=self.tdt, device=dev)
+            self._lin(taps[i], W8[f"proj{i}"], B * NP, c, D_, y, bias=P[h + f"projects.{i}.bias"])
+            proj.append(y)
+        f0 = self._convT(proj[0], W8["rs0"], B, ph, pw, 256, 256, 4, 4, 0, bias=P[h + "resize_layers.0.bias"])
+        f1 = self._convT(proj[1], W8["rs1"], B, ph, pw, 512, 512, 2, 2, 0, bias=P[h + "resize_layers.1.bias"])
+        f2 = proj[2]
+        f3 = self._conv(proj[3], W8["rs3"], B, ph, pw, 1024, 1024, 3, 2, 1, bias=P[h + "resize_layers.3.bias"])
+        feats = [f0, f1, f2, f3]
+        dims = [(f.shape[1], f.shape[2]) for f in feats]
+        rn = [self._conv(f, W8[f"rn{i + 1}"], B, dims[i][0], dims[i][1], f.shape[3], 256, 3, 1, 1) for i, f in enumerate(feats)]
+        if ctx is not None:
+            ctx.t["dec"] = dict(taps=taps, proj=proj, feats=feats, rn=rn, dims=dims)
+        p4 = self._fusion(4, rn[3], None, B, *dims[3], *dims[2], train, ctx)
+        p3 = self._fusion(3, p4, rn[2], B, *dims[2], *dims[1], train, ctx)
+        p2 = self._fusion(2, p3, rn[1], B, *dims[1], *dims[0], train, ctx)
+        p1 = self._fusion(1, p2, rn[0], B, *dims[0], 2 * dims[0][0], 2 * dims[0][1], train, ctx)
+        H1, W1 = p1.shape[1], p1.shape[2]
+        # classifier head: AdaptiveAvgPool2d(1) -> Linear -> ReLU -> Linear
+        pooled = torch.empty((B, 256), dtype=torch.float32, device=dev)
+        L("s3od_avgpool", dt, p1, pooled, B, H1 * W1, 256, st)
+        hid = torch.empty((B, 64), dtype=torch.float32, device=dev)
+        iou = torch.empty((B, 3), dtype=torch.float32, device=dev)
+        L("s3od_iou_head_fwd", pooled, P[h + "classifier_head.2.weight"], P[h + "classifier_head.2.bias"],
+          P[h + "classifier_head.4.weight"], P[h + "classifier_head.4.bias"], hid, iou, B, st)
+        # mask head (src/s3od/model.py:455-467)
+        m = h + "mask_head."
+        oc1 = self._conv(p1, W8["oc1"], B, H1, W1, 256, 128, 3, 1, 1, bias=P[m + "output_conv1.bias"])
+        up = self._convT(oc1, W8["up2x"], B, H1, W1, 128, 64, 4, 2, 1, bias=P[m + "upsample_2x.0.bias"], act=ACT_RELU)
+        HH, WW = up.shape[1], up.shape[2]
+        c64 = self._conv(up, W8["c64"], B, HH, WW, 64, 64, 3, 1, 1, bias=P[m + "upsample_2x.2.bias"], act=ACT_RELU)
+        # F.interpolate(size=(16ph,16pw), antialias=True) is an exact identity here (HH == 16*ph)
+        assert HH == 16 * ph and WW == 16 * pw
+        logits = torch.empty((B, 3, HH, WW), dtype=torch.float32, device=dev)
+        hsave = torch.empty((B * HH * WW, 96), dtype=self.tdt, device=dev) if ctx is not None else None
+        L("s3od_mask_heads_fwd", dt, B, HH, WW, c64, W8["heads1"], W8["heads1_b"], W8["heads2"], W8["heads2_b"],
+          logits, hsave, st)
+        if ctx is not None:
+            ctx.t["head"] = dict(p1=p1, pooled=pooled, hid=hid, oc1=oc1, up=up, c64=c64, hsave=hsave)
+        return {"pred_masks": logits, "pred_iou": iou, "features": p1.permute(0, 3, 1, 2)}
+
+    # ------------------------------------------------------------------ full forward
+    def forward(self, x, train=False, rope_rescale=None, ctx: Ctx | None = None):
+        """x: [B,3,H,W] fp32 CUDA (normalised image).  Returns the reference output dict."""
+        if x.dtype != torch.float32:
+            x = x.float()
+        x = x.contiguous()
+        self.prepare()
+        taps, (B, ph, pw, Nt) = self.encoder_forward(x, train, rope_rescale, ctx)
+        if ctx is not None:
+            ctx.B, ctx.H, ctx.W, ctx.ph, ctx.pw = B, x.shape[2], x.shape[3], ph, pw
+        return self.decoder_forward(taps, B, ph, pw, train, ctx)
