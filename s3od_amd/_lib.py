@@ -24,6 +24,7 @@ F32, BF16 = 0, 1
 _CT = {
     "int": ctypes.c_int, "long": ctypes.c_long, "float": ctypes.c_float, "double": ctypes.c_double,
     "void*": ctypes.c_void_p, "float*": ctypes.c_void_p, "double*": ctypes.c_void_p, "char*": ctypes.c_char_p,
+    "long*": ctypes.c_void_p, "int*": ctypes.c_void_p,
 }
 _DECL = re.compile(r"^(int|const char\*)\s+(s3od_\w+)\(([^)]*)\);", re.M)
 

@@ -1,0 +1,87 @@
+"""PyTorch autograd wiring for the native forward/backward.
+
+``dpt_train_forward`` runs the training forward (train-mode BatchNorm, sampled RoPE rescale)
+through ``DPTEngine`` and returns the reference output dict whose ``pred_masks`` / ``pred_iou``
+carry a grad_fn.  Its backward runs ``DPTEngine.backward``, which accumulates (fp32 atomics)
+straight into the model's flat gradient buffer; ``p.grad`` are views of that buffer, so
+gradient accumulation across micro-batches, ``zero_grad`` and optimizers behave as with the
+reference.  Parameters the reference never reaches (layer 11, final norm, mask_token,
+refinenet4.resConfUnit1) keep ``grad = None`` exactly like the reference.
+"""
+from __future__ import annotations
+
+import torch
+
+from .engine import Ctx
+
+
+class _DPTFn(torch.autograd.Function):
+    @staticmethod
+    def forward(fctx, x, anchor, model, eng, rescale):
+        ctx = Ctx()
+        out = eng.forward(x, train=True, rope_rescale=rescale, ctx=ctx)
+        fctx.s3od = (model, eng, ctx)
+        fctx.mark_non_differentiable(out["features"])
+        return out["pred_masks"], out["pred_iou"], out["features"]
+
+    @staticmethod
+    def backward(fctx, d_masks, d_iou, d_feat):
+        model, eng, ctx = fctx.s3od
+        G = model._grad_views()
+        if d_masks is None:
+            d_masks = torch.zeros((ctx.B, 3, 16 * ctx.ph, 16 * ctx.pw), dtype=torch.float32, device=G["_flat"].device)
+        if d_iou is None:
+            d_iou = torch.zeros((ctx.B, 3), dtype=torch.float32, device=G["_flat"].device)
+        eng.grad_hook = model._grad_ready_hook
+        try:
+            eng.backward(ctx, d_masks.float().contiguous(), d_iou.float().contiguous(), G)
+        finally:
+            eng.grad_hook = None
+            fctx.s3od = None
+        model._after_backward()
+        return None, torch.zeros((), device=d_iou.device), None, None, None
+
+
+def dpt_train_forward(model, eng, x):
+    rescale = model.sample_rope_rescale()
+    pm, iou, feat = _DPTFn.apply(x, model._autograd_anchor(), model, eng, rescale)
+    return {"pred_masks": pm, "pred_iou": iou, "features": feat}
+
+
+class _MaskLossFn(torch.autograd.Function):
+    """Fused multi-mask loss; returns (loss, packed parts)."""
+
+    @staticmethod
+    def forward(fctx, logits, pred_iou, masks, cfg):
+        from ._lib import lib, stream
+        B, M = logits.shape[:2]
+        HW = logits.shape[2] * logits.shape[3]
+        dev = logits.device
+        sums = torch.empty(B * M * 8, dtype=torch.float64, device=dev)
+        coef = torch.empty(B * M * 4, dtype=torch.float32, device=dev)
+        iou_ws = torch.empty(B * M * 2, dtype=torch.float32, device=dev)
+        diu = torch.empty(B * M, dtype=torch.float32, device=dev)
+        out = torch.empty(16 + B * M + B, dtype=torch.float32, device=dev)
+        logits = logits.contiguous()
+        masks = masks.contiguous().float()
+        lib()("s3od_mask_loss_fwd", logits, masks, pred_iou.contiguous().float(), B, M, HW, cfg["w_focal"], cfg["w_iou"],
+              cfg["w_bce"], cfg["w_mse"], cfg["lam"], 0.25, 2.0, sums, coef, iou_ws, diu, out, stream())
+        fctx.save_for_backward(logits, masks, coef, iou_ws, diu)
+        fctx.dims = (B, M, HW)
+        fctx.mark_non_differentiable(out)
+        return out[0], out
+
+    @staticmethod
+    def backward(fctx, g_loss, g_out):
+        from ._lib import lib, stream
+        logits, masks, coef, iou_ws, diu = fctx.saved_tensors
+        B, M, HW = fctx.dims
+        dl = torch.empty_like(logits)
+        di = torch.empty((B, M), dtype=torch.float32, device=logits.device)
+        g = g_loss.reshape(1).float().contiguous()
+        lib()("s3od_mask_loss_bwd", logits, masks, coef, iou_ws, diu, g, dl, di, B, M, HW, 0.25, 2.0, stream())
+        return dl, di, None, None
+
+
+def mask_loss(logits, pred_iou, masks, cfg):
+    return _MaskLossFn.apply(logits, pred_iou, masks, cfg)

@@ -219,6 +219,361 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const T* __restrict__ Q, 
   }
 }
 
+
+// ===================================================================================== backward
+// delta[bh][q] = sum_d dO[b][q][h*64+d] * O[b][q][h*64+d]
+template <typename T>
+__global__ void attn_delta_kernel(const T* __restrict__ O, const T* __restrict__ dO, float* __restrict__ delta, int N, int H, int BH) {
+  int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;   // row = bh*N + q
+  if (row >= BH * N) return;
+  int bh = row / N, q = row - bh * N, b = bh / H, h = bh - b * H;
+  long off = ((long)b * N + q) * (H * 64) + h * 64 + lane;
+  float v = to_f<T>(O[off]) * to_f<T>(dO[off]);
+  v = warp_sum(v);
+  if (lane == 0) delta[row] = v;
+}
+
+namespace {
+// 64-row x 64-d tile image used for both row reads (ds_read_b128 / scalar) and transposed reads
+template <typename T> struct Img;
+template <> struct Img<bf16> {
+  static constexpr int BYTES = 64 * 128;
+  DEV static int at(int row, int byte) { return row * 128 + ((((byte >> 4) ^ ((row >> 1) & 7)) << 4) | (byte & 15)); }
+};
+template <> struct Img<float> {
+  static constexpr int BYTES = 64 * 272;
+  DEV static int at(int row, int byte) { return row * 272 + byte; }
+};
+
+// stage a [64 rows][64] tile of a strided tensor (row stride ld elements) into registers / LDS
+template <typename T> struct RowTile {
+  static constexpr int CH = 64 * 64 * sizeof(T) / 16 / 256;
+  uint4 r[CH];
+  DEV void load(const T* base, long ld, int row0, int N, int tid) {
+#pragma unroll
+    for (int i = 0; i < CH; i++) {
+      int c = tid + 256 * i;
+      constexpr int CPR = 64 * sizeof(T) / 16;
+      int row = row0 + c / CPR, col = (c % CPR) * (16 / sizeof(T));
+      r[i] = row < N ? *(const uint4*)(base + (long)row * ld + col) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  DEV void store(char* lds, int tid) {
+#pragma unroll
+    for (int i = 0; i < CH; i++) {
+      int c = tid + 256 * i;
+      constexpr int CPR = 64 * sizeof(T) / 16;
+      *(uint4*)(lds + Img<T>::at(c / CPR, (c % CPR) * 16)) = r[i];
+    }
+  }
+};
+
+typedef __attribute__((address_space(3))) s16x4 lds_s4;
+// bf16 A/B fragment of a 16x32 block read TRANSPOSED from an Img<bf16>:
+// lane (g, i) gets X[row(g,j)][col0 + i] for j = 0..7 with row(g,j) = r0 + 4g + j (j<4), r0 + 16 + 4g + j-4 (j>=4)
+DEV bf16x8 tr_frag(const char* img, int r0, int col0, int lane) {
+  int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  int byte = (col0 + 4 * p) * 2;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + Img<bf16>::at(r0 + 4 * g + q, byte)));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + Img<bf16>::at(r0 + 16 + 4 * g + q, byte)));
+  bf16x4 a = __builtin_bit_cast(bf16x4, lo), b = __builtin_bit_cast(bf16x4, hi);
+  return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+// row fragment: lane (g, i) gets X[r0 + i][kk*32 + 8g .. +7]
+DEV bf16x8 row_frag(const char* img, int r0, int kk, int lane) {
+  return *(const bf16x8*)(img + Img<bf16>::at(r0 + (lane & 15), kk * 64 + (lane >> 4) * 16));
+}
+DEV bf16x8 pack8(f32x4 a, f32x4 b) {
+  return bf16x8{(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
+}
+DEV f32x4 mma_bf(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+DEV f32x4 mma_f(float a, float b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+DEV float ldsf(const char* img, int row, int col) { return *(const float*)(img + Img<float>::at(row, col * 4)); }
+}  // namespace
+
+// dK, dV.  Workgroup = 4 waves x 32 keys of one (b,h); loop over 64-query tiles.
+//   S  = Q K^T     (A = Q rows from LDS, B = K fragments in registers)   -> lane = key, regs = q
+//   dP = dO V^T    (A = dO rows from LDS, B = V fragments in registers)
+//   dV^T += dO^T P (A = dO^T via transposed LDS reads, B = P from the accumulators)
+//   dK^T += Q^T dS (A = Q^T via transposed LDS reads, B = dS from the accumulators)
+template <typename T>
+__global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
+                                                             const T* __restrict__ dO, const float* __restrict__ LSE,
+                                                             const float* __restrict__ Dl, T* __restrict__ dK, T* __restrict__ dV,
+                                                             int N, int H) {
+  constexpr bool F32 = std::is_same<T, float>::value;
+  typedef Img<T> I;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (2 * I::BYTES + 512)];
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
+  const T* Qp = Q + (long)bh * N * 64;
+  const T* Kp = K + (long)bh * N * 64;
+  const T* Vp = V + (long)bh * N * 64;
+  const T* dOp = dO + (long)b * N * (H * 64) + h * 64;
+  const long ldo = (long)H * 64;
+  const float* Lp = LSE + (long)bh * N;
+  const float* Dp = Dl + (long)bh * N;
+  const int k0 = blockIdx.x * 128 + wave * 32;
+
+  constexpr int KK = F32 ? 16 : 2;
+  typedef typename std::conditional<F32, float, bf16x8>::type frag;
+  frag kf[2][KK], vf[2][KK];
+#pragma unroll
+  for (int ks = 0; ks < 2; ks++) {
+    int key = k0 + ks * 16 + li;
+#pragma unroll
+    for (int kk = 0; kk < KK; kk++) {
+      if constexpr (F32) {
+        kf[ks][kk] = key < N ? Kp[(long)key * 64 + kk * 4 + g] : 0.f;
+        vf[ks][kk] = key < N ? Vp[(long)key * 64 + kk * 4 + g] : 0.f;
+      } else {
+        bf16x8 z; for (int e = 0; e < 8; e++) z[e] = (bf16)0.f;
+        kf[ks][kk] = key < N ? *(const bf16x8*)(Kp + (long)key * 64 + kk * 32 + 8 * g) : z;
+        vf[ks][kk] = key < N ? *(const bf16x8*)(Vp + (long)key * 64 + kk * 32 + 8 * g) : z;
+      }
+    }
+  }
+  f32x4 dk[4][2], dv[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int j = 0; j < 2; j++) { dk[i][j] = f32x4{0, 0, 0, 0}; dv[i][j] = f32x4{0, 0, 0, 0}; }
+
+  RowTile<T> tq, tdo;
+  float lse_r = 0.f, dl_r = 0.f;
+  const int nqt = (N + 63) / 64;
+  auto stage_load = [&](int qt) {
+    tq.load(Qp, 64, qt * 64, N, tid);
+    tdo.load(dOp, ldo, qt * 64, N, tid);
+    if (tid < 64) { int q = qt * 64 + tid; lse_r = q < N ? Lp[q] : INFINITY; dl_r = q < N ? Dp[q] : 0.f; }
+  };
+  auto stage_store = [&](char* base) {
+    tq.store(base, tid); tdo.store(base + I::BYTES, tid);
+    if (tid < 64) { ((float*)(base + 2 * I::BYTES))[tid] = lse_r; ((float*)(base + 2 * I::BYTES))[64 + tid] = dl_r; }
+  };
+  stage_load(0);
+  stage_store(smem);
+  __syncthreads();
+  int cur = 0;
+  constexpr int SB = 2 * I::BYTES + 512;
+  for (int qt = 0; qt < nqt; qt++) {
+    const bool more = qt + 1 < nqt;
+    if (more) stage_load(qt + 1);
+    const char* qs_ = smem + cur * SB;
+    const char* dos = qs_ + I::BYTES;
+    const float* lsel = (const float*)(qs_ + 2 * I::BYTES);
+    const float* dll = lsel + 64;
+    f32x4 s[4][2], dp[4][2];
+#pragma unroll
+    for (int qb = 0; qb < 4; qb++)
+#pragma unroll
+      for (int ks = 0; ks < 2; ks++) { s[qb][ks] = f32x4{0, 0, 0, 0}; dp[qb][ks] = f32x4{0, 0, 0, 0}; }
+#pragma unroll
+    for (int qb = 0; qb < 4; qb++) {
+#pragma unroll
+      for (int kk = 0; kk < KK; kk++) {
+        if constexpr (F32) {
+          float a = ldsf(qs_, qb * 16 + li, kk * 4 + g), c = ldsf(dos, qb * 16 + li, kk * 4 + g);
+#pragma unroll
+          for (int ks = 0; ks < 2; ks++) { s[qb][ks] = mma_f(a, kf[ks][kk], s[qb][ks]); dp[qb][ks] = mma_f(c, vf[ks][kk], dp[qb][ks]); }
+        } else {
+          bf16x8 a = row_frag(qs_, qb * 16, kk, lane), c = row_frag(dos, qb * 16, kk, lane);
+#pragma unroll
+          for (int ks = 0; ks < 2; ks++) { s[qb][ks] = mma_bf(a, kf[ks][kk], s[qb][ks]); dp[qb][ks] = mma_bf(c, vf[ks][kk], dp[qb][ks]); }
+        }
+      }
+    }
+    // P = exp(S - LSE[q]), dS = P*(dP - delta[q]);  q = qb*16 + 4g + i
+#pragma unroll
+    for (int qb = 0; qb < 4; qb++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        int qq = qb * 16 + 4 * g + i;
+        float L = lsel[qq], Dv = dll[qq];
+#pragma unroll
+        for (int ks = 0; ks < 2; ks++) {
+          float p = __expf(s[qb][ks][i] - L);
+          s[qb][ks][i] = p;
+          dp[qb][ks][i] = p * (dp[qb][ks][i] - Dv);
+        }
+      }
+    // dV^T += dO^T P ; dK^T += Q^T dS
+    if constexpr (F32) {
+#pragma unroll
+      for (int qb = 0; qb < 4; qb++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          int qq = qb * 16 + 4 * g + i;
+#pragma unroll
+          for (int ds = 0; ds < 4; ds++) {
+            float ao = ldsf(dos, qq, ds * 16 + li), aq = ldsf(qs_, qq, ds * 16 + li);
+#pragma unroll
+            for (int ks = 0; ks < 2; ks++) { dv[ds][ks] = mma_f(ao, s[qb][ks][i], dv[ds][ks]); dk[ds][ks] = mma_f(aq, dp[qb][ks][i], dk[ds][ks]); }
+          }
+        }
+    } else {
+#pragma unroll
+      for (int qst = 0; qst < 2; qst++) {
+        bf16x8 pb[2], sb[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ks++) { pb[ks] = pack8(s[2 * qst][ks], s[2 * qst + 1][ks]); sb[ks] = pack8(dp[2 * qst][ks], dp[2 * qst + 1][ks]); }
+#pragma unroll
+        for (int ds = 0; ds < 4; ds++) {
+          bf16x8 ao = tr_frag(dos, 32 * qst, ds * 16, lane), aq = tr_frag(qs_, 32 * qst, ds * 16, lane);
+#pragma unroll
+          for (int ks = 0; ks < 2; ks++) { dv[ds][ks] = mma_bf(ao, pb[ks], dv[ds][ks]); dk[ds][ks] = mma_bf(aq, sb[ks], dk[ds][ks]); }
+        }
+      }
+    }
+    if (more) stage_store(smem + (cur ^ 1) * SB);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // store: lane = key (li), rows d = ds*16 + 4g + i
+#pragma unroll
+  for (int ks = 0; ks < 2; ks++) {
+    int key = k0 + ks * 16 + li;
+    if (key >= N) continue;
+    T* dkr = dK + ((long)bh * N + key) * 64;
+    T* dvr = dV + ((long)bh * N + key) * 64;
+#pragma unroll
+    for (int ds = 0; ds < 4; ds++) {
+      int d = ds * 16 + 4 * g;
+      if constexpr (F32) {
+        *(float4*)(dkr + d) = make_float4(dk[ds][ks][0], dk[ds][ks][1], dk[ds][ks][2], dk[ds][ks][3]);
+        *(float4*)(dvr + d) = make_float4(dv[ds][ks][0], dv[ds][ks][1], dv[ds][ks][2], dv[ds][ks][3]);
+      } else {
+        *(bf16x4*)(dkr + d) = bf16x4{(bf16)dk[ds][ks][0], (bf16)dk[ds][ks][1], (bf16)dk[ds][ks][2], (bf16)dk[ds][ks][3]};
+        *(bf16x4*)(dvr + d) = bf16x4{(bf16)dv[ds][ks][0], (bf16)dv[ds][ks][1], (bf16)dv[ds][ks][2], (bf16)dv[ds][ks][3]};
+      }
+    }
+  }
+}
+
+// dQ (w.r.t. the pre-scaled q).  Workgroup = 4 waves x 32 queries; loop over 64-key tiles.
+//   S^T = K Q^T, dP^T = V dO^T (B operands Q, dO in registers)  -> lane = q, regs = keys
+//   dQ^T += K^T dS^T            (A = K^T via transposed LDS reads, B = dS^T from accumulators)
+template <typename T>
+__global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
+                                                           const T* __restrict__ dO, const float* __restrict__ LSE,
+                                                           const float* __restrict__ Dl, T* __restrict__ dQ, int N, int H) {
+  constexpr bool F32 = std::is_same<T, float>::value;
+  typedef Img<T> I;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * I::BYTES];
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
+  const T* Qp = Q + (long)bh * N * 64;
+  const T* Kp = K + (long)bh * N * 64;
+  const T* Vp = V + (long)bh * N * 64;
+  const T* dOp = dO + (long)b * N * (H * 64) + h * 64;
+  const long ldo = (long)H * 64;
+  const int q0 = blockIdx.x * 128 + wave * 32;
+  constexpr int KK = F32 ? 16 : 2;
+  typedef typename std::conditional<F32, float, bf16x8>::type frag;
+  frag qf[2][KK], of[2][KK];
+  float Lq[2], Dq[2];
+#pragma unroll
+  for (int qs = 0; qs < 2; qs++) {
+    int q = q0 + qs * 16 + li;
+    Lq[qs] = q < N ? LSE[(long)bh * N + q] : INFINITY;
+    Dq[qs] = q < N ? Dl[(long)bh * N + q] : 0.f;
+#pragma unroll
+    for (int kk = 0; kk < KK; kk++) {
+      if constexpr (F32) {
+        qf[qs][kk] = q < N ? Qp[(long)q * 64 + kk * 4 + g] : 0.f;
+        of[qs][kk] = q < N ? dOp[(long)q * ldo + kk * 4 + g] : 0.f;
+      } else {
+        bf16x8 z; for (int e = 0; e < 8; e++) z[e] = (bf16)0.f;
+        qf[qs][kk] = q < N ? *(const bf16x8*)(Qp + (long)q * 64 + kk * 32 + 8 * g) : z;
+        of[qs][kk] = q < N ? *(const bf16x8*)(dOp + (long)q * ldo + kk * 32 + 8 * g) : z;
+      }
+    }
+  }
+  f32x4 dq[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; i++) { dq[i][0] = f32x4{0, 0, 0, 0}; dq[i][1] = f32x4{0, 0, 0, 0}; }
+  RowTile<T> tk, tv;
+  const int nkt = (N + 63) / 64;
+  tk.load(Kp, 64, 0, N, tid); tv.load(Vp, 64, 0, N, tid);
+  tk.store(smem, tid); tv.store(smem + I::BYTES, tid);
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < nkt; kt++) {
+    const bool more = kt + 1 < nkt;
+    if (more) { tk.load(Kp, 64, (kt + 1) * 64, N, tid); tv.load(Vp, 64, (kt + 1) * 64, N, tid); }
+    const char* ks_ = smem + cur * 2 * I::BYTES;
+    const char* vs_ = ks_ + I::BYTES;
+    f32x4 s[4][2], dp[4][2];
+#pragma unroll
+    for (int kb = 0; kb < 4; kb++) {
+      s[kb][0] = s[kb][1] = dp[kb][0] = dp[kb][1] = f32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int kk = 0; kk < KK; kk++) {
+        if constexpr (F32) {
+          float a = ldsf(ks_, kb * 16 + li, kk * 4 + g), c = ldsf(vs_, kb * 16 + li, kk * 4 + g);
+#pragma unroll
+          for (int qs = 0; qs < 2; qs++) { s[kb][qs] = mma_f(a, qf[qs][kk], s[kb][qs]); dp[kb][qs] = mma_f(c, of[qs][kk], dp[kb][qs]); }
+        } else {
+          bf16x8 a = row_frag(ks_, kb * 16, kk, lane), c = row_frag(vs_, kb * 16, kk, lane);
+#pragma unroll
+          for (int qs = 0; qs < 2; qs++) { s[kb][qs] = mma_bf(a, qf[qs][kk], s[kb][qs]); dp[kb][qs] = mma_bf(c, of[qs][kk], dp[kb][qs]); }
+        }
+      }
+    }
+#pragma unroll
+    for (int kb = 0; kb < 4; kb++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        bool valid = kt * 64 + kb * 16 + 4 * g + i < N;
+#pragma unroll
+        for (int qs = 0; qs < 2; qs++) {
+          float p = valid ? __expf(s[kb][qs][i] - Lq[qs]) : 0.f;
+          dp[kb][qs][i] = p * (dp[kb][qs][i] - Dq[qs]);
+        }
+      }
+    if constexpr (F32) {
+#pragma unroll
+      for (int kb = 0; kb < 4; kb++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          int key = kb * 16 + 4 * g + i;
+#pragma unroll
+          for (int ds = 0; ds < 4; ds++) {
+            float a = ldsf(ks_, key, ds * 16 + li);
+            dq[ds][0] = mma_f(a, dp[kb][0][i], dq[ds][0]);
+            dq[ds][1] = mma_f(a, dp[kb][1][i], dq[ds][1]);
+          }
+        }
+    } else {
+#pragma unroll
+      for (int kst = 0; kst < 2; kst++) {
+        bf16x8 sb0 = pack8(dp[2 * kst][0], dp[2 * kst + 1][0]), sb1 = pack8(dp[2 * kst][1], dp[2 * kst + 1][1]);
+#pragma unroll
+        for (int ds = 0; ds < 4; ds++) {
+          bf16x8 a = tr_frag(ks_, 32 * kst, ds * 16, lane);
+          dq[ds][0] = mma_bf(a, sb0, dq[ds][0]);
+          dq[ds][1] = mma_bf(a, sb1, dq[ds][1]);
+        }
+      }
+    }
+    if (more) { tk.store(smem + (cur ^ 1) * 2 * I::BYTES, tid); tv.store(smem + (cur ^ 1) * 2 * I::BYTES + I::BYTES, tid); }
+    __syncthreads();
+    cur ^= 1;
+  }
+#pragma unroll
+  for (int qs = 0; qs < 2; qs++) {
+    int q = q0 + qs * 16 + li;
+    if (q >= N) continue;
+    T* r = dQ + ((long)bh * N + q) * 64;
+#pragma unroll
+    for (int ds = 0; ds < 4; ds++) {
+      int d = ds * 16 + 4 * g;
+      if constexpr (F32) *(float4*)(r + d) = make_float4(dq[ds][qs][0], dq[ds][qs][1], dq[ds][qs][2], dq[ds][qs][3]);
+      else *(bf16x4*)(r + d) = bf16x4{(bf16)dq[ds][qs][0], (bf16)dq[ds][qs][1], (bf16)dq[ds][qs][2], (bf16)dq[ds][qs][3]};
+    }
+  }
+}
+
 extern "C" {
 
 // q,k,v: [B*H, N, 64] (q pre-scaled by 1/8); o: [B, N, H*64]; lse: [B*H, N] fp32 (optional)
@@ -230,4 +585,20 @@ int s3od_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* 
   return s3od_check_launch("attn_fwd");
 }
 
+
+// backward: o, do: [B, N, H*64]; q,k,v: [B*H, N, 64]; lse, delta(workspace): [B*H, N] fp32
+// outputs dq (w.r.t. the 1/8-scaled q), dk, dv: [B*H, N, 64]
+int s3od_attn_bwd(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
+                  float* delta, void* dq, void* dk, void* dv, int B, int H, int N, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(cdiv(N, 128), B * H);
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL(attn_delta_kernel<T>, dim3(cdiv((long)B * H * N, 4)), dim3(256), 0, st, (const T*)o, (const T*)dout, delta, N, H, B * H);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<T>, grid, dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse, delta,
+                       (T*)dk, (T*)dv, N, H);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<T>, grid, dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse, delta,
+                       (T*)dq, N, H);
+  });
+  return s3od_check_launch("attn_bwd");
+}
 }  // extern "C"

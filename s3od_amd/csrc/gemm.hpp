@@ -220,7 +220,7 @@ template <typename T, int R> struct WgradB {
   static constexpr bool KCL = false;
   static constexpr int NCH = R / 32, EPC = 16 / sizeof(T), BK = KT<T>::BK;
   static constexpr int CPR = R * sizeof(T) / 16, RSTEP = 256 / CPR;
-  const T* x; ConvGeo g; int NPIX;   // g.SC = Cin of X, g.SH/SW = X dims, RH/RW = output grid
+  const T* x; ConvGeo g; int NPIX; int relu;   // g.SC = Cin of X, g.SH/SW = X dims, RH/RW = output grid
   int kr, kh, kw, cin; bool cval;
   int pb[NCH], py[NCH], pxx[NCH]; int started;
   DEV void setup(int t0, int tid) {
@@ -243,6 +243,7 @@ template <typename T, int R> struct WgradB {
       int iy = py[i] * g.s - g.p + kh, ix = pxx[i] * g.s - g.p + kw;
       bool ok = cval && pb[i] < g.B && iy >= 0 && iy < g.SH && ix >= 0 && ix < g.SW;
       v[i] = ok ? *(const uint4*)(x + (((long)pb[i] * g.SH + iy) * g.SW + ix) * g.SC + cin) : make_uint4(0, 0, 0, 0);
+      if (relu) v[i] = relu16<T>(v[i]);
       // advance by BK pixels
       pxx[i] += BK;
       while (pxx[i] >= g.RW) { pxx[i] -= g.RW; if (++py[i] >= g.RH) { py[i] = 0; pb[i]++; } }
@@ -415,12 +416,12 @@ template <class F> DEV void for_segments(const float* ct, int LDT, int BM, int B
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3, ACT_RELU_BWD = 4 };
 // ACT_GELU_BWD: o = v * gelu'(res1)   (res1 = saved pre-activation, not added)
 // ACT_RELU_BWD: o = v * (res1 > 0)    (res1 = saved activation output, not added)
-template <typename TO, typename TR> struct EpiStd {
+template <typename TO, typename TR, typename TP = TO> struct EpiStd {
   // pre = acc + bias[n] ;  v = pre*scale[n] + shift[n] ;  out = act(v) (+res1 +res2)
   TO* out; long ldo; int coff;          // output row stride / channel offset
   const float* bias; const float* scale; const float* shift;
   const TR* res1; long ldr1; const TR* res2; long ldr2;
-  TO* pre; long ldp;                    // optional: store pre (acc + bias)
+  TP* pre; long ldp;                    // optional: store pre (acc + bias), compute dtype
   double* stats;                        // optional: [2][N] (sum, sumsq) of pre (BN batch statistics)
   int act, M, N;
   RowMap rm;
@@ -431,7 +432,7 @@ template <typename TO, typename TR> struct EpiStd {
       long orow = rm.map(m);
 #pragma unroll
       for (int e = 0; e < 8; e++) { pv[e] = a[e] + (bias ? bias[n + e] : 0.f); v[e] = pv[e] * (scale ? scale[n + e] : 1.f) + (shift ? shift[n + e] : 0.f); }
-      if (pre) store8<TO>(pre + orow * ldp + n, pv);
+      if (pre) store8<TP>(pre + orow * ldp + n, pv);
       if (act >= ACT_GELU_BWD) {
         float r[8]; load8<TR>(res1 + orow * ldr1 + n, r);
 #pragma unroll

@@ -104,8 +104,8 @@ int s3od_linear_fwd(int dtype, int M, int N, int K, const void* x, long ldx, con
       constexpr int BM = 128, BN = 128;
       DenseKC<T, BM> la{(const T*)x, ldx, M, K, 0};
       DenseKC<T, BN> lb{(const T*)w, (long)K, N, K, 0};
-      EpiStd<TO, TR> e{(TO*)out, ldo, 0, bias, scale, shift, (const TR*)res1, ldr1, (const TR*)res2, ldr2,
-                       (TO*)pre, ldp, nullptr, act, M, N, rm};
+      EpiStd<TO, TR, T> e{(TO*)out, ldo, 0, bias, scale, shift, (const TR*)res1, ldr1, (const TR*)res2, ldr2,
+                          (T*)pre, ldp, nullptr, act, M, N, rm};
       return launch_igemm<T, BM, BN>(la, lb, e, M, N, KTILES, 1, 1, st);
     };
     if (out_f32 && res_f32) return go(0, float{}, float{});
@@ -116,10 +116,13 @@ int s3od_linear_fwd(int dtype, int M, int N, int K, const void* x, long ldx, con
   return 0;
 }
 
-// dx[m, n] = sum_k dy[m,k] w[k,n]  (w: [K=out][N=in]); act=ACT_GELU_BWD multiplies by gelu'(pre)
+// dx[rm(m), n] = sum_k dy[m,k] w[k,n] (+ res)  (w: [K=out][N=in]); act=ACT_GELU_BWD multiplies by
+// gelu'(aux); with act=ACT_NONE a non-null aux is ADDED (aux may alias dx: in-place accumulate).
 int s3od_linear_dgrad(int dtype, int M, int N, int K, const void* dy, long lddy, const void* w,
-                      int act, const void* aux, long ldaux, void* dx, long lddx, int out_f32, void* stream) {
+                      int act, const void* aux, long ldaux, void* dx, long lddx, int out_f32,
+                      int row_mode, int P, int prefix, void* stream) {
   S3OD_REQUIRE(K % 8 == 0 && N % 8 == 0, "linear_dgrad: K,N %% 8");
+  RowMap rm = dense_rm(); rm.mode = row_mode; rm.P = P; rm.prefix = prefix;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(K, KT<T>::BK);
@@ -127,10 +130,11 @@ int s3od_linear_dgrad(int dtype, int M, int N, int K, const void* dy, long lddy,
     DenseKC<T, BM> la{(const T*)dy, lddy, M, K, 0};
     DenseMC<T, BN> lb{(const T*)w, (long)N, K, N};
     if (out_f32) {
-      EpiStd<float, T> e{(float*)dx, lddx, 0, nullptr, nullptr, nullptr, (const T*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, dense_rm()};
+      // f32 output: aux is an f32 tensor to add (e.g. the residual-stream gradient, in place)
+      EpiStd<float, float> e{(float*)dx, lddx, 0, nullptr, nullptr, nullptr, (const float*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, rm};
       return launch_igemm<T, BM, BN>(la, lb, e, M, N, KTILES, 1, 1, st);
     }
-    EpiStd<T, T> e{(T*)dx, lddx, 0, nullptr, nullptr, nullptr, (const T*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, dense_rm()};
+    EpiStd<T, T> e{(T*)dx, lddx, 0, nullptr, nullptr, nullptr, (const T*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, rm};
     return launch_igemm<T, BM, BN>(la, lb, e, M, N, KTILES, 1, 1, st);
   });
   return 0;
@@ -204,7 +208,7 @@ int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int C
 int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW,
                     int stride, int pad, const void* dy, const void* wp,
                     const float* bias, const float* scale, const float* shift, int act, const void* res1,
-                    void* dx, void* pre, double* stats, void* stream) {
+                    const void* res2, void* dx, void* pre, double* stats, void* stream) {
   S3OD_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "conv_dgrad: channels %% 8");
   ConvGeo g0{}; g0.B = B; g0.SH = OH; g0.SW = OW; g0.SC = Cout; g0.KH = KH; g0.KW = KW; g0.s = stride; g0.p = pad;
   hipStream_t st = (hipStream_t)stream;
@@ -219,7 +223,7 @@ int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
           constexpr int BM = 128, BN = decltype(bn)::value;
           ConvDgradA<T, BM> la{}; la.dy = (const T*)dy; la.g = g; la.M = M;
           ConvDgradB<T, BN> lb{}; lb.w = (const T*)wp; lb.g = g; lb.NC = Cin;
-          EpiStd<T, T> e{(T*)dx, (long)Cin, 0, bias, scale, shift, (const T*)res1, (long)Cin, nullptr, 0,
+          EpiStd<T, T> e{(T*)dx, (long)Cin, 0, bias, scale, shift, (const T*)res1, (long)Cin, (const T*)res2, (long)Cin,
                          (T*)pre, (long)Cin, stats, act, M, N, rm};
           return launch_igemm<T, BM, BN>(la, lb, e, M, N, cdiv(K, KT<T>::BK), 1, 1, st);
         };
@@ -233,7 +237,7 @@ int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
 // conv wgrad: dw[Cout][Cin][KH][KW] (PyTorch layout, fp32) += sum_pix dy[pix][co] * x[src(pix,tap)][ci]
 // dy: [B,OH,OW,Cout]; x: [B,H,W,Cin].  Also serves ConvTranspose2d weights (conv view).
 int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW,
-                    int stride, int pad, const void* dy, const void* x, float* dw, int split, void* stream) {
+                    int stride, int pad, const void* dy, const void* x, int relu_x, float* dw, int split, void* stream) {
   S3OD_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "conv_wgrad: channels %% 8");
   ConvGeo g{}; g.B = B; g.SH = H; g.SW = W; g.SC = Cin; g.RH = OH; g.RW = OW; g.KH = KH; g.KW = KW; g.s = stride; g.p = pad;
   const int NPIX = B * OH * OW, M = Cout, N = KH * KW * Cin;
@@ -245,7 +249,7 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
       int sp = split;
       if (sp <= 0) { int tiles = cdiv(M, BM) * cdiv(N, BN); sp = max(1, min(KTILES / 8, 2048 / max(tiles, 1))); }
       DenseMC<T, BM> la{(const T*)dy, (long)Cout, NPIX, Cout};
-      WgradB<T, BN> lb{}; lb.x = (const T*)x; lb.g = g; lb.NPIX = NPIX;
+      WgradB<T, BN> lb{}; lb.x = (const T*)x; lb.g = g; lb.NPIX = NPIX; lb.relu = relu_x;
       EpiWgrad e{dw, M, N, Cin, KH * KW};
       return launch_igemm<T, BM, BN>(la, lb, e, M, N, KTILES, sp, 1, st);
     };

@@ -247,7 +247,23 @@ __global__ void qkv_unrope_kernel(const T* __restrict__ dq, const T* __restrict_
   store8<T>(dqkv + m * 2304 + which * 768 + h * 64 + d0, v);
 }
 
+// d(cls) = sum_b dx[b,0], d(reg[t]) = sum_b dx[b,1+t]  (accumulate)
+__global__ void token_prefix_bwd_kernel(const float* dx, float* dcls, float* dreg, int B, int Ntok) {
+  int t = blockIdx.x;  // 0..4
+  float* dst = t == 0 ? dcls : dreg + (t - 1) * 768;
+  for (int c = threadIdx.x; c < 768; c += blockDim.x) {
+    float s = 0.f;
+    for (int b = 0; b < B; b++) s += dx[((long)b * Ntok + t) * 768 + c];
+    dst[c] += s;
+  }
+}
+
 extern "C" {
+
+int s3od_token_prefix_bwd(const float* dx, float* dcls, float* dreg, int B, int Ntok, void* stream) {
+  hipLaunchKernelGGL(token_prefix_bwd_kernel, dim3(5), dim3(256), 0, (hipStream_t)stream, dx, dcls, dreg, B, Ntok);
+  return s3od_check_launch("token_prefix_bwd");
+}
 
 int s3od_patch_im2col(int dtype, const float* x, void* cols, int B, int H, int W, void* stream) {
   S3OD_REQUIRE(W % 4 == 0 && H >= 16 && W >= 16, "patch_im2col: W must be a multiple of 4 and H,W >= 16");

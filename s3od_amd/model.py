@@ -72,6 +72,9 @@ class DPTSegmentation(nn.Module):
                     own[k].copy_(torch.from_numpy(np.asarray(v)))
         self._engine = None
         self._rope_rescale = None   # train-mode RoPE rescale override (parity tests)
+        self._anchor = None
+        self._flat = None           # flat fp32 gradient buffer (see _grad_views)
+        self.grad_ready_callback = None   # fn(range_name, flat_slice) for bucketed all-reduce
 
     # ---------------------------------------------------------------- state dict
     def load_state_dict(self, state_dict, strict=True, assign=False):
@@ -93,6 +96,106 @@ class DPTSegmentation(nn.Module):
         if e.cdt != self.compute_dtype:
             e.set_dtype(self.compute_dtype)
         return e
+
+    # ---------------------------------------------------------------- gradients
+    def grad_layout(self):
+        """Flat gradient order: reference order with q/k/v weights and the three mask heads'
+        weights/biases made adjacent (they are produced by single fused kernels), encoder first.
+        Returns (list of (name, numel, shape), dict range_name -> (start, end))."""
+        from .weights import N_LAYERS
+        specs = [(n, sh) for n, sh, k in param_specs() if not (k.startswith("bn_") and k not in ("bn_w", "bn_b"))]
+        shapes = dict(specs)
+        unused = set(self.unused_parameter_names())
+        order = []
+        done = set()
+        for n, sh in specs:
+            if n in done or n in unused:
+                continue
+            if n.endswith("attention.k_proj.weight") or n.endswith("attention.v_proj.weight"):
+                continue
+            if n.endswith("attention.q_proj.weight"):
+                base = n[: -len("q_proj.weight")]
+                grp = [base + "q_proj.weight", base + "k_proj.weight", base + "v_proj.weight"]
+            elif ".mask_heads." in n:
+                m = "seg_head.mask_head.mask_heads."
+                grp = [m + f"{k}.{a}.{b}" for a, b in (("0", "weight"), ("0", "bias"), ("2", "weight"), ("2", "bias"))
+                       for k in range(3)]
+                grp = [g for g in grp if g not in done]
+            else:
+                grp = [n]
+            for g in grp:
+                order.append(g); done.add(g)
+        layout, ranges, off = [], {}, 0
+        for n in order:
+            numel = int(np.prod(shapes[n])) if shapes[n] else 1
+            layout.append((n, off, numel, shapes[n]))
+            key = "seg_head" if n.startswith("seg_head") else (
+                "layer" + n.split(".")[3] if n.startswith("encoder.model.layer.") else "embeddings")
+            a, b = ranges.get(key, (off, off))
+            ranges[key] = (min(a, off), off + numel)
+            off += numel
+        return layout, ranges, off
+
+    @staticmethod
+    def unused_parameter_names():
+        from .weights import N_LAYERS
+        last = N_LAYERS - 1
+        names = [n for n, sh, k in param_specs() if n.startswith(f"encoder.model.layer.{last}.")]
+        names += ["encoder.norm.weight", "encoder.norm.bias", "encoder.embeddings.mask_token"]
+        names += [n for n, sh, k in param_specs() if n.startswith("seg_head.scratch.refinenet4.resConfUnit1.")
+                  and not (k.startswith("bn_") and k not in ("bn_w", "bn_b"))]
+        return names
+
+    def _autograd_anchor(self):
+        dev = next(self.parameters()).device
+        if self._anchor is None or self._anchor.device != dev:
+            self._anchor = torch.zeros((), device=dev, requires_grad=True)
+        return self._anchor
+
+    def _grad_views(self):
+        """Make every reachable parameter's .grad a view of one flat fp32 buffer (zero-filled
+        where .grad was None) and return name -> grad view, plus the fused views the kernels use."""
+        params = dict(self.named_parameters())
+        dev = next(iter(params.values())).device
+        if self._flat is None or self._flat["buf"].device != dev:
+            layout, ranges, total = self.grad_layout()
+            self._flat = {"layout": layout, "ranges": ranges, "buf": torch.zeros(total, dtype=torch.float32, device=dev)}
+        fl = self._flat
+        buf = fl["buf"]
+        G = {"_flat": buf}
+        for n, off, numel, shape in fl["layout"]:
+            p = params[n]
+            v = buf[off:off + numel].view(shape)
+            g = p.grad
+            if g is None:
+                v.zero_()
+                p.grad = v
+            elif g.data_ptr() != v.data_ptr():
+                v.copy_(g)
+                p.grad = v
+            G[n] = v
+        pos = {n: off for n, off, numel, shape in fl["layout"]}
+        for i in range(11):
+            q = f"encoder.model.layer.{i}.attention."
+            o = pos[q + "q_proj.weight"]
+            G[f"qkv_w{i}"] = buf[o:o + 3 * 768 * 768]
+        m = "seg_head.mask_head.mask_heads."
+        for key, n, cnt in (("heads1_w", "0.0.weight", 96 * 64 * 9), ("heads1_b", "0.0.bias", 96),
+                            ("heads2_w", "0.2.weight", 96), ("heads2_b", "0.2.bias", 3)):
+            o = pos[m + n]
+            G[key] = buf[o:o + cnt]
+        return G
+
+    def _grad_ready_hook(self, name):
+        cb = self.grad_ready_callback
+        if cb is not None and self._flat is not None and name in self._flat["ranges"]:
+            a, b = self._flat["ranges"][name]
+            cb(name, self._flat["buf"][a:b])
+
+    def _after_backward(self):
+        cb = getattr(self, "grad_finish_callback", None)
+        if cb is not None:
+            cb()
 
     def sample_rope_rescale(self):
         """tf:…/modeling_dinov3_vit.py:124-150 with pos_embed_rescale=2.0: exp(U(-ln 2, ln 2))."""
