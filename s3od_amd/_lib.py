@@ -56,6 +56,7 @@ class _Lib:
         self.lib = ctypes.CDLL(str(LIB_PATH))
         self.decls = parse_header()
         self.fns = {}
+        self.timers = {}     # name -> list of (start, end) events recorded around each call
         for name, (ret, types) in self.decls.items():
             fn = getattr(self.lib, name)
             fn.argtypes = [_CT[t] for t in types]
@@ -79,7 +80,15 @@ class _Lib:
                     cargs.append(int(a))
             else:
                 cargs.append(a)
-        rc = fn(*cargs)
+        tm = self.timers.get(name) if self.timers else None
+        if tm is not None:
+            e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            rc = fn(*cargs)
+            e1.record()
+            tm.append((e0, e1))
+        else:
+            rc = fn(*cargs)
         if rc != 0:
             raise HipLibError(f"{name} failed (rc={rc}): {self.last_error()}")
         return rc

@@ -90,6 +90,7 @@ __global__ void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restri
   load8<float>(mean + c, mu); load8<float>(rstd + c, rs);
   float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   long p0 = (long)blockIdx.x * pix_per_block, p1 = min(npix, p0 + pix_per_block);
+#pragma unroll 4
   for (long p = p0 + ri; p < p1; p += rows) {
     float d[8], zz[8];
     load8<T>(dy + p * C + c, d); load8<T>(z + p * C + c, zz);
@@ -208,6 +209,7 @@ __global__ void avgpool_kernel(const T* __restrict__ x, float* __restrict__ out,
   const int b = blockIdx.y, c = cgi * 8;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   long p0 = (long)blockIdx.x * pix_per_block, p1 = min((long)HW, p0 + pix_per_block);
+#pragma unroll 4
   for (long p = p0 + ri; p < p1; p += rows) {
     float v[8]; load8<T>(x + ((long)b * HW + p) * C + c, v);
 #pragma unroll
@@ -275,6 +277,7 @@ __global__ void mask_heads_bwd_kernel(const float* __restrict__ dlog, const T* _
   const float wk = w2[t];
   float accw = 0.f, accb = 0.f;
   long p0 = (long)blockIdx.x * pix_per_block, p1 = min(M, p0 + pix_per_block);
+#pragma unroll 4
   for (long m = p0; m < p1; m++) {
     int b = m / HW; long pix = m - (long)b * HW;
     float dl = dlog[((long)b * 3 + k) * HW + pix];
@@ -325,7 +328,7 @@ int s3od_bn_bwd(int dtype, const void* dy, const void* z, const void* y_relu, co
   S3OD_REQUIRE(C % 8 == 0 && 256 % (C / 8) == 0, "bn_bwd: C");
   hipStream_t st = (hipStream_t)stream;
   (void)hipMemsetAsync(sums, 0, sizeof(double) * 2 * C, st);
-  const int ppb = 2048;
+  const int ppb = 4096;
   DISPATCH_T(dtype, {
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(cdiv(npix, ppb)), dim3(256), 0, st, (const T*)dy, (const T*)z, (const T*)y_relu,
                        mean, rstd, sums, npix, C, ppb);
@@ -359,7 +362,7 @@ int s3od_avgpool(int dtype, const void* x, float* out, int B, int HW, int C, voi
   S3OD_REQUIRE(C % 8 == 0 && 256 % (C / 8) == 0, "avgpool: C");
   hipStream_t st = (hipStream_t)stream;
   (void)hipMemsetAsync(out, 0, sizeof(float) * B * C, st);
-  const int ppb = 4096;
+  const int ppb = 1024;
   DISPATCH_T(dtype, {
     hipLaunchKernelGGL(avgpool_kernel<T>, dim3(cdiv(HW, ppb), B), dim3(256), 0, st, (const T*)x, out, HW, C, ppb);
   });
@@ -382,7 +385,7 @@ int s3od_iou_head_bwd(const float* pooled, const float* hid, const float* w1, co
 int s3od_mask_heads_bwd(int dtype, const float* dlogits, const void* hsave, const float* w2, void* dh, float* dw2, float* db2,
                         int B, int HW, void* stream) {
   long M = (long)B * HW;
-  const int ppb = 1024;
+  const int ppb = 128;
   DISPATCH_T(dtype, {
     hipLaunchKernelGGL(mask_heads_bwd_kernel<T>, dim3(cdiv(M, ppb)), dim3(96), 0, (hipStream_t)stream, dlogits, (const T*)hsave, w2,
                        (T*)dh, dw2, db2, M, HW, ppb);

@@ -21,6 +21,8 @@
 #pragma once
 #include "common.hpp"
 
+constexpr int GEMM_THREADS = 512;          // 8 waves per workgroup (2 per SIMD)
+constexpr int GEMM_WAVES = GEMM_THREADS / 64;
 template <typename T> struct KT { static constexpr int BK = 64; };
 template <> struct KT<float> { static constexpr int BK = 32; };
 
@@ -85,172 +87,240 @@ template <typename T> DEV uint4 relu16(uint4 v) {
 }
 
 // ------------------------------------------------------------------ operand loaders
-// Each loader fills NCH = R/32 16-byte chunks per thread for K tile kt.
-// KC: chunk i of thread t -> row (t>>3) + 32 i, byte (t&7)*16 of the 128-B k-row.
-// MC: chunk i of thread t -> k-row t/CPR + i*(256/CPR), 16-B column chunk t%CPR.
+// Global -> LDS by LDS-DMA (global_load_lds_dwordx4): one wave instruction writes 1 KiB of LDS
+// lane-linearly (wave base + lane*16), so the XOR swizzles are applied to the per-lane SOURCE
+// address (guide §5.4 rule 21).  Out-of-range chunks (padding, tails) read a zero page.
+// A tile of R rows is R*128 bytes: NIW = R*128/1024/GEMM_WAVES = R/64 instructions per wave.
+//   KC image: instruction slot o = (wave*NIW + i)*1024 + lane*16 -> row o>>7, physical 16-B slot
+//             (o>>4)&7, logical chunk = phys ^ ((row>>1)&7)
+//   MC image: k-row o / RB, physical byte o % RB, logical 32-B slot = phys32 ^ g(k)
+__device__ __attribute__((aligned(16))) uint4 g_s3od_zero[8];
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glob_void;
+DEV void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((glob_void*)src, (lds_void*)lds_wave_base, 16, 0, 0);
+}
+DEV const void* zero_src() { return (const void*)g_s3od_zero; }
+
+template <int RB> DEV int mc_logical_byte(int k, int phys) {
+  constexpr int SLOTS = RB / 32;
+  int g = ((k & 3) | (((k >> 3) & 1) << 2)) & (SLOTS - 1);
+  return (((phys >> 5) ^ g) << 5) | (phys & 31);
+}
+
+template <typename T, int R> struct KCGeom {
+  static constexpr int NIW = R * 128 / 1024 / GEMM_WAVES, EPC = 16 / sizeof(T), BK = KT<T>::BK;
+  static_assert(NIW >= 1, "tile too small for the wave count");
+  // row and logical element offset (within the k tile) of this lane's chunk of instruction i
+  DEV static int row(int wave, int i, int lane) { return (wave * NIW + i) * 8 + (lane >> 3); }
+  DEV static int kel(int wave, int i, int lane) { int r = row(wave, i, lane); return ((lane & 7) ^ ((r >> 1) & 7)) * EPC; }
+};
+template <typename T, int R> struct MCGeom {
+  static constexpr int NIW = R * 128 / 1024 / GEMM_WAVES, RB = R * sizeof(T), BK = KT<T>::BK;
+  DEV static int krow(int wave, int i, int lane) { return ((wave * NIW + i) * 1024 + lane * 16) / RB; }
+  DEV static int col(int wave, int i, int lane) {
+    int o = ((wave * NIW + i) * 1024 + lane * 16) % RB;
+    return mc_logical_byte<RB>(krow(wave, i, lane), o) / (int)sizeof(T);
+  }
+};
 
 template <typename T, int R> struct DenseKC {          // X[row*ld + k]
-  static constexpr bool KCL = true;
-  static constexpr int NCH = R / 32, EPC = 16 / sizeof(T), BK = KT<T>::BK;
+  static constexpr bool KCL = true, RELU = false;
+  typedef KCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* p; long ld; int nrows, K; int relu;
-  const T* rowp[NCH]; int koff;
+  const T* rowp[NIW]; int kel[NIW]; bool rv[NIW];
   DEV void setup(int t0, int tid) {
-    koff = (tid & 7) * EPC;
+    const int lane = tid & 63, wave = tid >> 6;
 #pragma unroll
-    for (int i = 0; i < NCH; i++) { int r = t0 + (tid >> 3) + 32 * i; rowp[i] = r < nrows ? p + (long)r * ld : nullptr; }
+    for (int i = 0; i < NIW; i++) {
+      int r = t0 + G::row(wave, i, lane);
+      rv[i] = r < nrows;
+      rowp[i] = p + (long)(rv[i] ? r : 0) * ld;
+      kel[i] = G::kel(wave, i, lane);
+    }
   }
-  DEV void load(int kt, uint4* v) {
-    int k = kt * BK + koff;
+  DEV void issue(int kt, char* tile) {
+    const int wave = threadIdx.x >> 6;
 #pragma unroll
-    for (int i = 0; i < NCH; i++) {
-      v[i] = (rowp[i] && k < K) ? *(const uint4*)(rowp[i] + k) : make_uint4(0, 0, 0, 0);
-      if (relu) v[i] = relu16<T>(v[i]);
+    for (int i = 0; i < NIW; i++) {
+      int k = kt * BK + kel[i];
+      const void* src = (rv[i] && k < K) ? (const void*)(rowp[i] + k) : zero_src();
+      glds16(src, tile + (wave * NIW + i) * 1024);
     }
   }
 };
 
 template <typename T, int R> struct DenseMC {          // X[k*ld + col]
-  static constexpr bool KCL = false;
-  static constexpr int NCH = R / 32, EPC = 16 / sizeof(T), BK = KT<T>::BK;
-  static constexpr int CPR = R * sizeof(T) / 16, RSTEP = 256 / CPR;
+  static constexpr bool KCL = false, RELU = false;
+  typedef MCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* p; long ld; int K, ncols;
-  int col, kr; bool cval;
-  DEV void setup(int t0, int tid) { col = t0 + (tid % CPR) * EPC; kr = tid / CPR; cval = col < ncols; }
-  DEV void load(int kt, uint4* v) {
+  int relu = 0;
+  int kr[NIW], cl[NIW];
+  DEV void setup(int t0, int tid) {
+    const int lane = tid & 63, wave = tid >> 6;
 #pragma unroll
-    for (int i = 0; i < NCH; i++) {
-      int k = kt * BK + kr + i * RSTEP;
-      v[i] = (cval && k < K) ? *(const uint4*)(p + (long)k * ld + col) : make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < NIW; i++) { kr[i] = G::krow(wave, i, lane); cl[i] = t0 + G::col(wave, i, lane); }
+  }
+  DEV void issue(int kt, char* tile) {
+    const int wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < NIW; i++) {
+      int k = kt * BK + kr[i];
+      const void* src = (k < K && cl[i] < ncols) ? (const void*)(p + (long)k * ld + cl[i]) : zero_src();
+      glds16(src, tile + (wave * NIW + i) * 1024);
     }
   }
 };
 
 // conv forward A operand: rows = output pixels (b,oy,ox) of RH x RW, k = tap*SC + c
-template <typename T, int R> struct ConvFwdA {
-  static constexpr bool KCL = true;
-  static constexpr int NCH = R / 32, EPC = 16 / sizeof(T), BK = KT<T>::BK;
+template <typename T, int R, bool RELU_ = false> struct ConvFwdA {
+  static constexpr bool KCL = true, RELU = RELU_;
+  typedef KCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* x; ConvGeo g; int M; int relu;
-  int rb[NCH], ry[NCH], rx[NCH];
-  int tap, c;     // incremental k -> (tap, channel) state of this thread's chunk
+  int rb[NIW], ry[NIW], rx[NIW];
+  int tap[NIW], c[NIW];     // incremental k -> (tap, channel) per chunk
   DEV void setup(int t0, int tid) {
+    const int lane = tid & 63, wave = tid >> 6;
     int hw = g.RH * g.RW;
 #pragma unroll
-    for (int i = 0; i < NCH; i++) {
-      int m = t0 + (tid >> 3) + 32 * i;
+    for (int i = 0; i < NIW; i++) {
+      int m = t0 + G::row(wave, i, lane);
       if (m < M) { int b = m / hw; int r = m - b * hw; int oy = r / g.RW; rb[i] = b; ry[i] = oy * g.s - g.p; rx[i] = (r - oy * g.RW) * g.s - g.p; }
       else { rb[i] = -1; ry[i] = 0; rx[i] = 0; }
+      tap[i] = -1; c[i] = G::kel(wave, i, lane);
     }
-    tap = -1;
   }
-  DEV void load(int kt, uint4* v) {
-    int koff = (threadIdx.x & 7) * EPC;
-    if (tap < 0) { int k = kt * BK + koff; tap = k / g.SC; c = k - tap * g.SC; }
-    int kh = tap / g.KW, kw = tap - kh * g.KW;
-    bool kval = tap < g.KH * g.KW;
+  DEV void issue(int kt, char* tile) {
+    const int wave = threadIdx.x >> 6;
 #pragma unroll
-    for (int i = 0; i < NCH; i++) {
+    for (int i = 0; i < NIW; i++) {
+      if (tap[i] < 0) { int k = kt * BK + c[i]; tap[i] = k / g.SC; c[i] = k - tap[i] * g.SC; }
+      int kh = tap[i] / g.KW, kw = tap[i] - kh * g.KW;
       int iy = ry[i] + kh, ix = rx[i] + kw;
-      bool ok = kval && rb[i] >= 0 && iy >= 0 && iy < g.SH && ix >= 0 && ix < g.SW;
-      v[i] = ok ? *(const uint4*)(x + (((long)rb[i] * g.SH + iy) * g.SW + ix) * g.SC + c) : make_uint4(0, 0, 0, 0);
-      if (relu) v[i] = relu16<T>(v[i]);
+      bool ok = tap[i] < g.KH * g.KW && rb[i] >= 0 && iy >= 0 && iy < g.SH && ix >= 0 && ix < g.SW;
+      const void* src = ok ? (const void*)(x + (((long)rb[i] * g.SH + iy) * g.SW + ix) * g.SC + c[i]) : zero_src();
+      glds16(src, tile + (wave * NIW + i) * 1024);
+      c[i] += BK; while (c[i] >= g.SC) { c[i] -= g.SC; tap[i]++; }
     }
-    c += BK; while (c >= g.SC) { c -= g.SC; tap++; }
   }
 };
 
 // dgrad / ConvT A operand: rows = class pixels (b, y', x'), k = (jh*ntw + jw)*SC + c
 template <typename T, int R> struct ConvDgradA {
-  static constexpr bool KCL = true;
-  static constexpr int NCH = R / 32, EPC = 16 / sizeof(T), BK = KT<T>::BK;
+  static constexpr bool KCL = true, RELU = false;
+  typedef KCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* dy; ConvGeo g; int M;
-  int rb[NCH], ry[NCH], rx[NCH];
-  int tap, c;
+  int relu = 0;
+  int rb[NIW], ry[NIW], rx[NIW];
+  int tap[NIW], c[NIW];
   DEV void setup(int t0, int tid) {
+    const int lane = tid & 63, wave = tid >> 6;
     int hw = g.RH * g.RW;
 #pragma unroll
-    for (int i = 0; i < NCH; i++) {
-      int m = t0 + (tid >> 3) + 32 * i;
+    for (int i = 0; i < NIW; i++) {
+      int m = t0 + G::row(wave, i, lane);
       if (m < M) { int b = m / hw; int r = m - b * hw; int yy = r / g.RW; rb[i] = b; ry[i] = yy + g.qy0; rx[i] = (r - yy * g.RW) + g.qx0; }
       else { rb[i] = -1; ry[i] = 0; rx[i] = 0; }
+      tap[i] = -1; c[i] = G::kel(wave, i, lane);
     }
-    tap = -1;
   }
-  DEV void load(int kt, uint4* v) {
-    int koff = (threadIdx.x & 7) * EPC;
-    if (tap < 0) { int k = kt * BK + koff; tap = k / g.SC; c = k - tap * g.SC; }
-    int jh = g.ntw ? tap / g.ntw : 0, jw = tap - jh * g.ntw;
-    bool kval = tap < g.nth * g.ntw;
+  DEV void issue(int kt, char* tile) {
+    const int wave = threadIdx.x >> 6;
 #pragma unroll
-    for (int i = 0; i < NCH; i++) {
+    for (int i = 0; i < NIW; i++) {
+      if (tap[i] < 0) { int k = kt * BK + c[i]; tap[i] = k / g.SC; c[i] = k - tap[i] * g.SC; }
+      int jh = g.ntw ? tap[i] / g.ntw : 0, jw = tap[i] - jh * g.ntw;
       int sy = ry[i] - jh, sx = rx[i] - jw;
-      bool ok = kval && rb[i] >= 0 && sy >= 0 && sy < g.SH && sx >= 0 && sx < g.SW;
-      v[i] = ok ? *(const uint4*)(dy + (((long)rb[i] * g.SH + sy) * g.SW + sx) * g.SC + c) : make_uint4(0, 0, 0, 0);
+      bool ok = tap[i] < g.nth * g.ntw && rb[i] >= 0 && sy >= 0 && sy < g.SH && sx >= 0 && sx < g.SW;
+      const void* src = ok ? (const void*)(dy + (((long)rb[i] * g.SH + sy) * g.SW + sx) * g.SC + c[i]) : zero_src();
+      glds16(src, tile + (wave * NIW + i) * 1024);
+      c[i] += BK; while (c[i] >= g.SC) { c[i] -= g.SC; tap[i]++; }
     }
-    c += BK; while (c >= g.SC) { c -= g.SC; tap++; }
   }
 };
 
 // dgrad / ConvT B operand (MC): B[k=(jh,jw,c)][n] = W[c][kh0+s*jh][kw0+s*jw][n], W repacked [C][KH][KW][N]
 template <typename T, int R> struct ConvDgradB {
-  static constexpr bool KCL = false;
-  static constexpr int NCH = R / 32, EPC = 16 / sizeof(T), BK = KT<T>::BK;
-  static constexpr int CPR = R * sizeof(T) / 16, RSTEP = 256 / CPR;
+  static constexpr bool KCL = false, RELU = false;
+  typedef MCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* w; ConvGeo g; int NC;     // NC = output channels of the dgrad (= conv input channels)
-  int col, kr; bool cval;
-  DEV void setup(int t0, int tid) { col = t0 + (tid % CPR) * EPC; kr = tid / CPR; cval = col < NC; }
-  DEV void load(int kt, uint4* v) {
-    int K = g.nth * g.ntw * g.SC;
+  int relu = 0;
+  int kr[NIW], cl[NIW];
+  DEV void setup(int t0, int tid) {
+    const int lane = tid & 63, wave = tid >> 6;
 #pragma unroll
-    for (int i = 0; i < NCH; i++) {
-      int k = kt * BK + kr + i * RSTEP;
-      uint4 r = make_uint4(0, 0, 0, 0);
-      if (cval && k < K) {
-        int t = k / g.SC, c = k - t * g.SC;
+    for (int i = 0; i < NIW; i++) { kr[i] = G::krow(wave, i, lane); cl[i] = t0 + G::col(wave, i, lane); }
+  }
+  DEV void issue(int kt, char* tile) {
+    const int wave = threadIdx.x >> 6;
+    const int K = g.nth * g.ntw * g.SC;
+#pragma unroll
+    for (int i = 0; i < NIW; i++) {
+      int k = kt * BK + kr[i];
+      const void* src = zero_src();
+      if (k < K && cl[i] < NC) {
+        int t = k / g.SC, cc = k - t * g.SC;
         int jh = t / g.ntw, jw = t - jh * g.ntw;
         int kh = g.kh0 + g.s * jh, kw = g.kw0 + g.s * jw;
-        r = *(const uint4*)(w + (((long)c * g.KH + kh) * g.KW + kw) * NC + col);
+        src = (const void*)(w + (((long)cc * g.KH + kh) * g.KW + kw) * NC + cl[i]);
       }
-      v[i] = r;
+      glds16(src, tile + (wave * NIW + i) * 1024);
     }
   }
 };
 
 // wgrad B operand (MC gather): B[k=pix of the conv output grid RH x RW][n=(tap, cin)] = X[src][cin]
-template <typename T, int R> struct WgradB {
-  static constexpr bool KCL = false;
-  static constexpr int NCH = R / 32, EPC = 16 / sizeof(T), BK = KT<T>::BK;
-  static constexpr int CPR = R * sizeof(T) / 16, RSTEP = 256 / CPR;
+template <typename T, int R, bool RELU_ = false> struct WgradB {
+  static constexpr bool KCL = false, RELU = RELU_;
+  typedef MCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* x; ConvGeo g; int NPIX; int relu;   // g.SC = Cin of X, g.SH/SW = X dims, RH/RW = output grid
-  int kr, kh, kw, cin; bool cval;
-  int pb[NCH], py[NCH], pxx[NCH]; int started;
+  int kh[NIW], kw[NIW], cin[NIW], kr[NIW]; bool cval[NIW];
+  int pb[NIW], py[NIW], pxx[NIW]; int started;
   DEV void setup(int t0, int tid) {
-    int col = t0 + (tid % CPR) * EPC; kr = tid / CPR;
-    int tap = col / g.SC; cin = col - tap * g.SC; kh = tap / g.KW; kw = tap - kh * g.KW;
-    cval = tap < g.KH * g.KW; started = 0;
+    const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int i = 0; i < NIW; i++) {
+      int col = t0 + G::col(wave, i, lane);
+      kr[i] = G::krow(wave, i, lane);
+      int tp = col / g.SC; cin[i] = col - tp * g.SC; kh[i] = tp / g.KW; kw[i] = tp - kh[i] * g.KW;
+      cval[i] = tp < g.KH * g.KW;
+    }
+    started = 0;
   }
-  DEV void load(int kt, uint4* v) {
+  DEV void issue(int kt, char* tile) {
+    const int wave = threadIdx.x >> 6;
     if (!started) {
       started = 1;
+      const int hw = g.RH * g.RW;
 #pragma unroll
-      for (int i = 0; i < NCH; i++) {
-        int k = kt * BK + kr + i * RSTEP; int hw = g.RH * g.RW;
+      for (int i = 0; i < NIW; i++) {
+        int k = kt * BK + kr[i];
         int b = k / hw; int r = k - b * hw; int oy = r / g.RW;
         pb[i] = b; py[i] = oy; pxx[i] = r - oy * g.RW;
       }
     }
 #pragma unroll
-    for (int i = 0; i < NCH; i++) {
-      int iy = py[i] * g.s - g.p + kh, ix = pxx[i] * g.s - g.p + kw;
-      bool ok = cval && pb[i] < g.B && iy >= 0 && iy < g.SH && ix >= 0 && ix < g.SW;
-      v[i] = ok ? *(const uint4*)(x + (((long)pb[i] * g.SH + iy) * g.SW + ix) * g.SC + cin) : make_uint4(0, 0, 0, 0);
-      if (relu) v[i] = relu16<T>(v[i]);
-      // advance by BK pixels
+    for (int i = 0; i < NIW; i++) {
+      int iy = py[i] * g.s - g.p + kh[i], ix = pxx[i] * g.s - g.p + kw[i];
+      bool ok = cval[i] && pb[i] < g.B && iy >= 0 && iy < g.SH && ix >= 0 && ix < g.SW;
+      const void* src = ok ? (const void*)(x + (((long)pb[i] * g.SH + iy) * g.SW + ix) * g.SC + cin[i]) : zero_src();
+      glds16(src, tile + (wave * NIW + i) * 1024);
       pxx[i] += BK;
       while (pxx[i] >= g.RW) { pxx[i] -= g.RW; if (++py[i] >= g.RH) { py[i] = 0; pb[i]++; } }
     }
     (void)NPIX;
   }
 };
+
+DEV bf16x8 relu_frag(bf16x8 v) {
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  u4 w = __builtin_bit_cast(u4, v);
+#pragma unroll
+  for (int i = 0; i < 4; i++) { unsigned m = (w[i] >> 15) & 0x00010001u; w[i] &= ~(m * 0xFFFFu); }
+  return __builtin_bit_cast(bf16x8, w);
+}
+DEV float relu_frag(float v) { return fmaxf(v, 0.f); }
 
 // ------------------------------------------------------------------ fragment readers
 template <typename T, bool KCL, int R> struct Frag;
@@ -306,27 +376,52 @@ template <> struct Mma<float> {
 };
 
 // ------------------------------------------------------------------ the kernel
-template <typename T, int BM, int BN> struct GemmShape {
+template <typename T, int BM, int BN, int NST_ = 3> struct GemmShape {
   static constexpr int BK = KT<T>::BK;
   static constexpr int ABYTES = BM * 128, BBYTES = BN * 128;
   static constexpr int STAGE = ABYTES + BBYTES;
+  static constexpr int NST = NST_;
   static constexpr int LDT = BN + 4;                       // fp32 C-tile row stride
   static constexpr int CBYTES = BM * LDT * 4;
-  static constexpr int LDS = (2 * STAGE > CBYTES ? 2 * STAGE : CBYTES);
+  static constexpr int LDS = (NST * STAGE > CBYTES ? NST * STAGE : CBYTES);
+  // wave grid: 8 waves as WM x WN
+  static constexpr int WM = BM >= 2 * BN ? 4 : (BN >= 2 * BM ? 2 : (BM >= BN ? 4 : 2));
+  static constexpr int WN = GEMM_WAVES / WM;
+  static constexpr int TM = BM / WM, TN = BN / WN;         // per-wave tile
+  static constexpr int MI = TM / 16, NI = TN / 16;
+  static_assert(MI >= 1 && NI >= 1 && TM % 16 == 0 && TN % 16 == 0, "bad wave tiling");
 };
 
 struct KRange { int kt0, kt1; };
 
-// Block-level epilogue contract:  epi(tile, LDT, m0, n0, tid)
-template <typename T, int BM, int BN, class LA, class LB, class EPI>
-__global__ void __launch_bounds__(256) igemm_kernel(LA la, LB lb, EPI epi, int KTILES, int split) {
-  typedef GemmShape<T, BM, BN> S;
+template <int N> DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+DEV void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Block-level epilogue contract:  epi(tile, LDT, m0, n0, tid, BM, BN)
+//
+// Main loop: 3 LDS stages filled by LDS-DMA two K-tiles ahead; one raw s_barrier per K tile,
+// placed BEFORE the last k-step's MFMAs so the next tile's first fragments are read from LDS
+// while the current tile's last MFMAs run (fragments double-buffered in registers).
+// vmcnt is counted (the tile two steps ahead stays in flight across the barrier); there is
+// no __syncthreads() in the loop (it would drain vmcnt to 0: guide §5).
+// Block order is remapped so consecutive tiles of one row-panel share an XCD (guide T1).
+template <typename T, int BM, int BN, int NST, class LA, class LB, class EPI>
+__global__ void __launch_bounds__(GEMM_THREADS) igemm_kernel(LA la, LB lb, EPI epi, int KTILES, int split) {
+  typedef GemmShape<T, BM, BN, NST> S;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  constexpr int MI = BM / 32, NI = BN / 32;   // 16x16 blocks per wave
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  // split-K range
+  const int wm = wave / S::WN, wn = wave % S::WN;
+  constexpr int MI = S::MI, NI = S::NI, KS = Mma<T>::KSTEPS;
+  constexpr int NL = LA::NIW + LB::NIW;       // LDS-DMA instructions per thread per K tile
+  int bx, by;
+  {
+    const int nwg = gridDim.x * gridDim.y;
+    const int L = blockIdx.y * gridDim.x + blockIdx.x;
+    const int q = nwg >> 3, r = nwg & 7, xcd = L & 7, idx = L >> 3;
+    const int W = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+    bx = W % gridDim.x; by = W / gridDim.x;
+  }
+  const int m0 = by * BM, n0 = bx * BN;
   int per = (KTILES + split - 1) / split;
   int kt0 = blockIdx.z * per, kt1 = min(KTILES, kt0 + per);
   epi.prepare(blockIdx.z);
@@ -339,60 +434,80 @@ __global__ void __launch_bounds__(256) igemm_kernel(LA la, LB lb, EPI epi, int K
 #pragma unroll
     for (int j = 0; j < NI; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[LA::NCH], rb[LB::NCH];
-  auto stage_store = [&](char* base) {
-    char* la_ = base; char* lb_ = base + S::ABYTES;
+  typedef typename Mma<T>::frag frag;
+  frag fa[2][MI], fb[2][NI];
+  auto read_frags = [&](int buf, const char* stage, int kk) {
+    const char* As = stage;
+    const char* Bs = stage + S::ABYTES;
 #pragma unroll
-    for (int i = 0; i < LA::NCH; i++) {
-      int off;
-      if constexpr (LA::KCL) off = kc_off((tid >> 3) + 32 * i, (tid & 7) * 16);
-      else { constexpr int CPR = BM * sizeof(T) / 16; off = mc_off<BM * sizeof(T)>(tid / CPR + i * (256 / CPR), (tid % CPR) * 16); }
-      *(uint4*)(la_ + off) = ra[i];
+    for (int i = 0; i < MI; i++) fa[buf][i] = Frag<T, LA::KCL, BM>::read(As, wm * S::TM + i * 16, kk, lane);
+#pragma unroll
+    for (int j = 0; j < NI; j++) fb[buf][j] = Frag<T, LB::KCL, BN>::read(Bs, wn * S::TN + j * 16, kk, lane);
+  };
+  auto mfmas = [&](int buf) {
+    if constexpr (LA::RELU) {
+#pragma unroll
+      for (int i = 0; i < MI; i++) fa[buf][i] = relu_frag(fa[buf][i]);
+    }
+    if constexpr (LB::RELU) {
+#pragma unroll
+      for (int j = 0; j < NI; j++) fb[buf][j] = relu_frag(fb[buf][j]);
     }
 #pragma unroll
-    for (int i = 0; i < LB::NCH; i++) {
-      int off;
-      if constexpr (LB::KCL) off = kc_off((tid >> 3) + 32 * i, (tid & 7) * 16);
-      else { constexpr int CPR = BN * sizeof(T) / 16; off = mc_off<BN * sizeof(T)>(tid / CPR + i * (256 / CPR), (tid % CPR) * 16); }
-      *(uint4*)(lb_ + off) = rb[i];
-    }
+    for (int i = 0; i < MI; i++)
+#pragma unroll
+      for (int j = 0; j < NI; j++) acc[i][j] = Mma<T>::mma(fa[buf][i], fb[buf][j], acc[i][j]);
   };
 
-  if (kt0 < kt1) {
-    la.load(kt0, ra); lb.load(kt0, rb);
-    stage_store(smem);
-    __syncthreads();
+  const int nt = kt1 - kt0;
+  constexpr int PD = NST - 1;                 // LDS-DMA prefetch distance (tiles in flight)
+  if (nt > 0) {
+    // prologue: tiles 0 .. PD-1
+#pragma unroll
+    for (int q = 0; q < PD; q++)
+      if (q < nt) { la.issue(kt0 + q, smem + q * S::STAGE); lb.issue(kt0 + q, smem + q * S::STAGE + S::ABYTES); }
+    if constexpr (PD == 2) { if (nt > 1) wait_vmcnt<NL>(); else wait_vmcnt<0>(); }
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    read_frags(0, smem, 0);
     int cur = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const bool more = kt + 1 < kt1;
-      if (more) { la.load(kt + 1, ra); lb.load(kt + 1, rb); }
-      const char* As = smem + cur * S::STAGE;
-      const char* Bs = As + S::ABYTES;
-#pragma unroll
-      for (int kk = 0; kk < Mma<T>::KSTEPS; kk++) {
-        typename Mma<T>::frag af[MI], bfr[NI];
-#pragma unroll
-        for (int i = 0; i < MI; i++) af[i] = Frag<T, LA::KCL, BM>::read(As, wm * (BM / 2) + i * 16, kk, lane);
-#pragma unroll
-        for (int j = 0; j < NI; j++) bfr[j] = Frag<T, LB::KCL, BN>::read(Bs, wn * (BN / 2) + j * 16, kk, lane);
-#pragma unroll
-        for (int i = 0; i < MI; i++)
-#pragma unroll
-          for (int j = 0; j < NI; j++) acc[i][j] = Mma<T>::mma(af[i], bfr[j], acc[i][j]);
+    for (int t = 0; t < nt; ++t) {
+      const bool pre = t + PD < nt;
+      if (pre) {
+        int st = cur + PD; if (st >= NST) st -= NST;
+        char* nx = smem + st * S::STAGE;
+        la.issue(kt0 + t + PD, nx);
+        lb.issue(kt0 + t + PD, nx + S::ABYTES);
       }
-      if (more) stage_store(smem + (cur ^ 1) * S::STAGE);
-      __syncthreads();
-      cur ^= 1;
+      const char* stg = smem + cur * S::STAGE;
+      int nxt = cur + 1; if (nxt >= NST) nxt -= NST;
+#pragma unroll
+      for (int kk = 0; kk < KS; kk++) {
+        const int b = kk & 1;
+        if (kk + 1 < KS) {
+          read_frags(b ^ 1, stg, kk + 1);
+        } else if (t + 1 < nt) {
+          // tile t+1 landed (own DMAs): PD-1 newer tiles may stay in flight
+          if constexpr (PD == 2) { if (pre) wait_vmcnt<NL>(); else wait_vmcnt<0>(); }
+          else wait_vmcnt<0>();
+          wait_lgkm0();
+          __builtin_amdgcn_s_barrier();
+          read_frags(b ^ 1, smem + nxt * S::STAGE, 0);
+        }
+        mfmas(b);
+      }
+      cur = nxt;
     }
   }
+  __syncthreads();
   // stage C tile to LDS (fp32)
   float* ct = (float*)smem;
 #pragma unroll
   for (int i = 0; i < MI; i++)
 #pragma unroll
     for (int j = 0; j < NI; j++) {
-      int r = wm * (BM / 2) + i * 16 + (lane >> 4) * 4;
-      int c = wn * (BN / 2) + j * 16 + (lane & 15);
+      int r = wm * S::TM + i * 16 + (lane >> 4) * 4;
+      int c = wn * S::TN + j * 16 + (lane & 15);
 #pragma unroll
       for (int e = 0; e < 4; e++) ct[(r + e) * S::LDT + c] = acc[i][j][e];
     }
@@ -403,7 +518,7 @@ __global__ void __launch_bounds__(256) igemm_kernel(LA la, LB lb, EPI epi, int K
 // iterate 8-wide row segments of the staged tile: f(m, n, const float* v8)
 template <class F> DEV void for_segments(const float* ct, int LDT, int BM, int BN, int m0, int n0, int M, int N, int tid, F f) {
   const int segs = BM * BN / 8, spr = BN / 8;
-  for (int s = tid; s < segs; s += 256) {
+  for (int s = tid; s < segs; s += GEMM_THREADS) {
     int r = s / spr, cs = s - r * spr;
     int m = m0 + r, n = n0 + cs * 8;
     if (m < M && n < N) f(m, n, ct + r * LDT + cs * 8, r, cs * 8);
@@ -451,7 +566,7 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
     });
     if (stats) {
       // column statistics of pre over this tile's valid rows: 256 threads -> (col, row-phase)
-      int nph = 256 / BN;
+      int nph = GEMM_THREADS / BN;
       int c = tid % BN, ph = tid / BN;
       int n = n0 + c;
       if (n < N) {
@@ -476,7 +591,7 @@ struct EpiWgrad {
   DEV void prepare(int) {}
   DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN) const {
     const int total = BM * BN;
-    for (int s = tid; s < total; s += 256) {
+    for (int s = tid; s < total; s += GEMM_THREADS) {
       int r = s / BN, c = s - r * BN;
       int m = m0 + r, n = n0 + c;
       if (m < M && n < N) {
@@ -487,13 +602,13 @@ struct EpiWgrad {
   }
 };
 
-template <typename T, int BM, int BN, class LA, class LB, class EPI>
+template <typename T, int BM, int BN, class LA, class LB, class EPI, int NST = 3>
 static int launch_igemm(LA la, LB lb, EPI epi, int M, int N, int KTILES, int split, int zdim_extra, hipStream_t st) {
-  typedef GemmShape<T, BM, BN> S;
-  auto kfn = igemm_kernel<T, BM, BN, LA, LB, EPI>;
+  typedef GemmShape<T, BM, BN, NST> S;
+  auto kfn = igemm_kernel<T, BM, BN, NST, LA, LB, EPI>;
   static bool attr = false;
   if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS); attr = true; }
   dim3 grid(cdiv(N, BN), cdiv(M, BM), split * zdim_extra);
-  hipLaunchKernelGGL(kfn, grid, dim3(256), S::LDS, st, la, lb, epi, KTILES, split);
+  hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), S::LDS, st, la, lb, epi, KTILES, split);
   return s3od_check_launch("igemm");
 }

@@ -11,6 +11,28 @@
 
 static RowMap dense_rm() { RowMap r{}; r.mode = 0; return r; }
 
+// Tile configuration (dev knob for the micro-benchmarks): S3OD_GEMM_CFG=<n> forces one config for
+// every GEMM entry point; default (-1) = per-op choice below.
+//   0: 256x128, 3 stages (1 WG/CU)   1: 128x128, 2 stages (2 WG/CU)   2: 128x128, 3 stages
+//   3: 256x128, 2 stages (BN is clamped to 64 for 64-channel convs: 256x64 x 2 stages = 80 KB)
+#include <stdlib.h>
+static int gemm_cfg() {
+  static int c = -2;
+  if (c == -2) { const char* e = getenv("S3OD_GEMM_CFG"); c = e ? atoi(e) : -1; }
+  return c;
+}
+template <int BM_, int BN_, int NST_> struct TileCfg { static constexpr int BM = BM_, BN = BN_, NST = NST_; };
+// call f(TileCfg) for the selected config; `def` = per-op default config index
+template <class F> static int with_cfg(int def, F f) {
+  int c = gemm_cfg(); if (c < 0) c = def;
+  switch (c) {
+    case 1: return f(TileCfg<128, 128, 2>{});
+    case 2: return f(TileCfg<128, 128, 3>{});
+    case 3: return f(TileCfg<256, 128, 2>{});
+    default: return f(TileCfg<256, 128, 3>{});
+  }
+}
+
 // ------------------------------------------------------------------ QKV + RoPE epilogue
 // n in [0,2304): q | k | v ; RoPE on patch tokens for q,k (tf:…/modeling_dinov3_vit.py:238-268);
 // q pre-multiplied by the softmax scale 1/8 (exact in any binary float format).
@@ -57,7 +79,7 @@ template <typename T> struct EpiHeads {
   DEV void prepare(int) {}
   DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN) const {
     float* t = (float*)ct;  // relu in place
-    for (int s = tid; s < BM * 96; s += 256) {
+    for (int s = tid; s < BM * 96; s += GEMM_THREADS) {
       int r = s / 96, c = s - r * 96;
       t[r * LDT + c] = fmaxf(t[r * LDT + c] + b1[c], 0.f);
     }
@@ -67,7 +89,7 @@ template <typename T> struct EpiHeads {
         store8<T>(hsave + (long)m * 96 + n, a);
       });
     }
-    for (int s = tid; s < 3 * BM; s += 256) {
+    for (int s = tid; s < 3 * BM; s += GEMM_THREADS) {
       int k = s / BM, r = s - k * BM;
       int m = m0 + r;
       if (m >= M) continue;
@@ -101,12 +123,14 @@ int s3od_linear_fwd(int dtype, int M, int N, int K, const void* x, long ldx, con
     const int KTILES = cdiv(K, KT<T>::BK);
     auto go = [&](auto tile, auto tout, auto tres) -> int {
       typedef decltype(tout) TO; typedef decltype(tres) TR;
-      constexpr int BM = 128, BN = 128;
-      DenseKC<T, BM> la{(const T*)x, ldx, M, K, 0};
-      DenseKC<T, BN> lb{(const T*)w, (long)K, N, K, 0};
-      EpiStd<TO, TR, T> e{(TO*)out, ldo, 0, bias, scale, shift, (const TR*)res1, ldr1, (const TR*)res2, ldr2,
-                          (T*)pre, ldp, nullptr, act, M, N, rm};
-      return launch_igemm<T, BM, BN>(la, lb, e, M, N, KTILES, 1, 1, st);
+      return with_cfg(K >= 2048 ? 0 : 1, [&](auto C) -> int {
+        constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
+        DenseKC<T, BM> la{(const T*)x, ldx, M, K, 0};
+        DenseKC<T, BN> lb{(const T*)w, (long)K, N, K, 0};
+        EpiStd<TO, TR, T> e{(TO*)out, ldo, 0, bias, scale, shift, (const TR*)res1, ldr1, (const TR*)res2, ldr2,
+                            (T*)pre, ldp, nullptr, act, M, N, rm};
+        return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, KTILES, 1, 1, st);
+      });
     };
     if (out_f32 && res_f32) return go(0, float{}, float{});
     if (out_f32) return go(0, float{}, T{});
@@ -126,16 +150,18 @@ int s3od_linear_dgrad(int dtype, int M, int N, int K, const void* dy, long lddy,
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(K, KT<T>::BK);
-    constexpr int BM = 128, BN = 128;
-    DenseKC<T, BM> la{(const T*)dy, lddy, M, K, 0};
-    DenseMC<T, BN> lb{(const T*)w, (long)N, K, N};
-    if (out_f32) {
-      // f32 output: aux is an f32 tensor to add (e.g. the residual-stream gradient, in place)
-      EpiStd<float, float> e{(float*)dx, lddx, 0, nullptr, nullptr, nullptr, (const float*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, rm};
-      return launch_igemm<T, BM, BN>(la, lb, e, M, N, KTILES, 1, 1, st);
-    }
-    EpiStd<T, T> e{(T*)dx, lddx, 0, nullptr, nullptr, nullptr, (const T*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, rm};
-    return launch_igemm<T, BM, BN>(la, lb, e, M, N, KTILES, 1, 1, st);
+    return with_cfg(1, [&](auto C) -> int {
+      constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
+      DenseKC<T, BM> la{(const T*)dy, lddy, M, K, 0};
+      DenseMC<T, BN> lb{(const T*)w, (long)N, K, N};
+      if (out_f32) {
+        // f32 output: aux is an f32 tensor to add (e.g. the residual-stream gradient, in place)
+        EpiStd<float, float> e{(float*)dx, lddx, 0, nullptr, nullptr, nullptr, (const float*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, rm};
+        return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, KTILES, 1, 1, st);
+      }
+      EpiStd<T, T> e{(T*)dx, lddx, 0, nullptr, nullptr, nullptr, (const T*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, rm};
+      return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, KTILES, 1, 1, st);
+    });
   });
   return 0;
 }
@@ -147,15 +173,15 @@ int s3od_linear_wgrad(int dtype, int Nout, int Kin, int rows, const void* dy, lo
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(rows, KT<T>::BK);
-    if (split <= 0) {
-      int tiles = cdiv(Nout, 128) * cdiv(Kin, 128);
-      split = max(1, min(KTILES / 8, 2048 / max(tiles, 1)));
-    }
-    constexpr int BM = 128, BN = 128;
-    DenseMC<T, BM> la{(const T*)dy, lddy, rows, Nout};
-    DenseMC<T, BN> lb{(const T*)x, ldx, rows, Kin};
-    EpiWgrad e{dw, Nout, Kin, Kin, 1};
-    return launch_igemm<T, BM, BN>(la, lb, e, Nout, Kin, KTILES, split, 1, st);
+    return with_cfg(1, [&](auto C) -> int {
+      constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
+      int sp = split;
+      if (sp <= 0) { int tiles = cdiv(Nout, BM) * cdiv(Kin, BN); sp = max(1, min(KTILES / 8, 2048 / max(tiles, 1))); }
+      DenseMC<T, BM> la{(const T*)dy, lddy, rows, Nout};
+      DenseMC<T, BN> lb{(const T*)x, ldx, rows, Kin};
+      EpiWgrad e{dw, Nout, Kin, Kin, 1};
+      return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, Nout, Kin, KTILES, sp, 1, st);
+    });
   });
   return 0;
 }
@@ -166,11 +192,13 @@ int s3od_qkv_rope_fwd(int dtype, int B, int Ntok, int P, const void* x, const vo
   const int H = 12, D = 768, N = 3 * D, M = B * Ntok;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
-    constexpr int BM = 128, BN = 128;
-    DenseKC<T, BM> la{(const T*)x, (long)D, M, D, 0};
-    DenseKC<T, BN> lb{(const T*)w, (long)D, N, D, 0};
-    EpiQKV<T> e{(T*)q, (T*)k, (T*)v, bias, cos_t, sin_t, M, Ntok, P, H};
-    return launch_igemm<T, BM, BN>(la, lb, e, M, N, cdiv(D, KT<T>::BK), 1, 1, st);
+    return with_cfg(1, [&](auto C) -> int {
+      constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
+      DenseKC<T, BM> la{(const T*)x, (long)D, M, D, 0};
+      DenseKC<T, BN> lb{(const T*)w, (long)D, N, D, 0};
+      EpiQKV<T> e{(T*)q, (T*)k, (T*)v, bias, cos_t, sin_t, M, Ntok, P, H};
+      return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, cdiv(D, KT<T>::BK), 1, 1, st);
+    });
   });
   return 0;
 }
@@ -189,16 +217,23 @@ int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int C
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(K, KT<T>::BK);
-    auto go = [&](auto bn) -> int {
-      constexpr int BM = 128, BN = decltype(bn)::value;
-      ConvFwdA<T, BM> la{}; la.x = (const T*)x; la.g = g; la.M = M; la.relu = relu_in;
-      DenseKC<T, BN> lb{(const T*)wp, (long)K, N, K, 0};
-      EpiStd<T, T> e{(T*)out, (long)Cout, 0, bias, scale, shift, (const T*)res1, (long)Cout, (const T*)res2, (long)Cout,
-                     (T*)pre, (long)Cout, stats, act, M, N, dense_rm()};
-      return launch_igemm<T, BM, BN>(la, lb, e, M, N, KTILES, 1, 1, st);
+    auto go = [&](auto bn, auto rl) -> int {
+      return with_cfg(Cout <= 64 ? 3 : 1, [&](auto C) -> int {
+        constexpr int BM = decltype(C)::BM, NST = decltype(C)::NST;
+        constexpr int BN = decltype(bn)::value < decltype(C)::BN ? decltype(bn)::value : decltype(C)::BN;
+        ConvFwdA<T, BM, decltype(rl)::value> la{}; la.x = (const T*)x; la.g = g; la.M = M; la.relu = relu_in;
+        DenseKC<T, BN> lb{(const T*)wp, (long)K, N, K, 0};
+        EpiStd<T, T> e{(T*)out, (long)Cout, 0, bias, scale, shift, (const T*)res1, (long)Cout, (const T*)res2, (long)Cout,
+                       (T*)pre, (long)Cout, stats, act, M, N, dense_rm()};
+        return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, KTILES, 1, 1, st);
+      });
     };
-    if (Cout <= 64) return go(std::integral_constant<int, 64>{});
-    return go(std::integral_constant<int, 128>{});
+    if (relu_in) {
+      if (Cout <= 64) return go(std::integral_constant<int, 64>{}, std::true_type{});
+      return go(std::integral_constant<int, 128>{}, std::true_type{});
+    }
+    if (Cout <= 64) return go(std::integral_constant<int, 64>{}, std::false_type{});
+    return go(std::integral_constant<int, 128>{}, std::false_type{});
   });
   return 0;
 }
@@ -220,12 +255,15 @@ int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
         if (M == 0) continue;
         RowMap rm{}; rm.mode = 2; rm.RH = g.RH; rm.RW = g.RW; rm.OH = H; rm.OW = W; rm.s = stride; rm.py = py; rm.px = px;
         auto go = [&](auto bn) -> int {
-          constexpr int BM = 128, BN = decltype(bn)::value;
-          ConvDgradA<T, BM> la{}; la.dy = (const T*)dy; la.g = g; la.M = M;
-          ConvDgradB<T, BN> lb{}; lb.w = (const T*)wp; lb.g = g; lb.NC = Cin;
-          EpiStd<T, T> e{(T*)dx, (long)Cin, 0, bias, scale, shift, (const T*)res1, (long)Cin, (const T*)res2, (long)Cin,
-                         (T*)pre, (long)Cin, stats, act, M, N, rm};
-          return launch_igemm<T, BM, BN>(la, lb, e, M, N, cdiv(K, KT<T>::BK), 1, 1, st);
+          return with_cfg(Cin <= 64 ? 3 : 1, [&](auto C) -> int {
+            constexpr int BM = decltype(C)::BM, NST = decltype(C)::NST;
+            constexpr int BN = decltype(bn)::value < decltype(C)::BN ? decltype(bn)::value : decltype(C)::BN;
+            ConvDgradA<T, BM> la{}; la.dy = (const T*)dy; la.g = g; la.M = M;
+            ConvDgradB<T, BN> lb{}; lb.w = (const T*)wp; lb.g = g; lb.NC = Cin;
+            EpiStd<T, T> e{(T*)dx, (long)Cin, 0, bias, scale, shift, (const T*)res1, (long)Cin, (const T*)res2, (long)Cin,
+                           (T*)pre, (long)Cin, stats, act, M, N, rm};
+            return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, cdiv(K, KT<T>::BK), 1, 1, st);
+          });
         };
         int rc = Cin <= 64 ? go(std::integral_constant<int, 64>{}) : go(std::integral_constant<int, 128>{});
         if (rc) return rc;
@@ -244,17 +282,21 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(NPIX, KT<T>::BK);
-    auto go = [&](auto bm) -> int {
-      constexpr int BM = decltype(bm)::value, BN = 128;
+    auto go = [&](auto bm, auto rl) -> int {
+      constexpr int BM = decltype(bm)::value, BN = 128, NST = 2;
       int sp = split;
       if (sp <= 0) { int tiles = cdiv(M, BM) * cdiv(N, BN); sp = max(1, min(KTILES / 8, 2048 / max(tiles, 1))); }
       DenseMC<T, BM> la{(const T*)dy, (long)Cout, NPIX, Cout};
-      WgradB<T, BN> lb{}; lb.x = (const T*)x; lb.g = g; lb.NPIX = NPIX; lb.relu = relu_x;
+      WgradB<T, BN, decltype(rl)::value> lb{}; lb.x = (const T*)x; lb.g = g; lb.NPIX = NPIX; lb.relu = relu_x;
       EpiWgrad e{dw, M, N, Cin, KH * KW};
-      return launch_igemm<T, BM, BN>(la, lb, e, M, N, KTILES, sp, 1, st);
+      return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, KTILES, sp, 1, st);
     };
-    if (Cout <= 64) return go(std::integral_constant<int, 64>{});
-    return go(std::integral_constant<int, 128>{});
+    if (relu_x) {
+      if (Cout <= 64) return go(std::integral_constant<int, 64>{}, std::true_type{});
+      return go(std::integral_constant<int, 128>{}, std::true_type{});
+    }
+    if (Cout <= 64) return go(std::integral_constant<int, 64>{}, std::false_type{});
+    return go(std::integral_constant<int, 128>{}, std::false_type{});
   });
   return 0;
 }

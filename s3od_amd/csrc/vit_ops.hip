@@ -170,19 +170,45 @@ __global__ void cast_tap_kernel(const float* __restrict__ x, T* __restrict__ y, 
 }
 
 // column sums of a [M, N] T matrix (bias gradients): out[n] += sum_m a[m, n]
+// block = 256 threads = tpr column-groups (8 columns each) x rp row phases; LDS reduction over
+// the row phases, one fp32 atomic per column per block.
 template <typename T>
-__global__ void colsum_kernel(const T* __restrict__ a, long lda, int M, int N, float* __restrict__ out, int rows_per_block) {
-  int n = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  if (n >= N) return;
-  int r0 = blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
+__global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ a, long lda, int M, int N, float* __restrict__ out,
+                                                     int rows_per_block) {
+  __shared__ float red[256 * 8];
+  const int G = N / 8;
+  const int tpr = G < 256 ? G : 256, rp = 256 / tpr;
+  const int t = threadIdx.x, ci = t % tpr, ph = t / tpr;
+  const int cg = blockIdx.x * tpr + ci;
+  const bool act = ph < rp && cg < G;
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int r = r0; r < r1; r++) {
-    float v[8]; load8<T>(a + (long)r * lda + n, v);
+  if (act) {
+    long r0 = (long)blockIdx.y * rows_per_block, r1 = min((long)M, r0 + rows_per_block);
+    const T* base = a + cg * 8;
+    long r = r0 + ph;
+    for (; r + 3 * rp < r1; r += 4 * rp) {     // 4 independent 16-B loads in flight per thread
+      float v0[8], v1[8], v2[8], v3[8];
+      load8<T>(base + r * lda, v0); load8<T>(base + (r + rp) * lda, v1);
+      load8<T>(base + (r + 2 * rp) * lda, v2); load8<T>(base + (r + 3 * rp) * lda, v3);
 #pragma unroll
-    for (int e = 0; e < 8; e++) s[e] += v[e];
+      for (int e = 0; e < 8; e++) s[e] += (v0[e] + v1[e]) + (v2[e] + v3[e]);
+    }
+    for (; r < r1; r += rp) {
+      float v[8]; load8<T>(base + r * lda, v);
+#pragma unroll
+      for (int e = 0; e < 8; e++) s[e] += v[e];
+    }
   }
 #pragma unroll
-  for (int e = 0; e < 8; e++) atomicAdd(out + n + e, s[e]);
+  for (int e = 0; e < 8; e++) red[t * 8 + e] = s[e];
+  __syncthreads();
+  if (ph == 0 && cg < G) {
+    for (int q = 1; q < rp; q++)
+#pragma unroll
+      for (int e = 0; e < 8; e++) s[e] += red[(q * tpr + ci) * 8 + e];
+#pragma unroll
+    for (int e = 0; e < 8; e++) atomicAdd(out + cg * 8 + e, s[e]);
+  }
 }
 
 // LayerScale backward: du = dx * lam (T); dlam[n] += sum_m dx*u ; dbias[n] += sum_m du
@@ -194,6 +220,7 @@ __global__ void scale_bwd_kernel(const float* __restrict__ dx, const T* __restri
   int r0 = blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
   float l[8]; load8<float>(lam + n, l);
   float sl[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 4
   for (int r = r0; r < r1; r++) {
     float d[8], uu[8], o[8];
     load8<float>(dx + (long)r * 768 + n, d);
@@ -311,10 +338,11 @@ int s3od_cast_tap(int dtype, const float* x, void* y, int B, int Ntok, int P, vo
 
 int s3od_colsum(int dtype, const void* a, long lda, int M, int N, float* out, void* stream) {
   S3OD_REQUIRE(N % 8 == 0, "colsum: N %% 8");
-  const int rpb = 256;
-  dim3 grid(cdiv(N / 8, 256), cdiv(M, rpb));
+  const int G = N / 8, tpr = G < 256 ? G : 256, gx = cdiv(G, tpr);
+  long rpb = max(64L, (long)M * gx / 2048);
+  dim3 grid(gx, cdiv(M, rpb));
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(colsum_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)a, lda, M, N, out, rpb);
+    hipLaunchKernelGGL(colsum_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)a, lda, M, N, out, (int)rpb);
   });
   return s3od_check_launch("colsum");
 }

@@ -146,6 +146,17 @@ class DPTSegmentation(nn.Module):
                   and not (k.startswith("bn_") and k not in ("bn_w", "bn_b"))]
         return names
 
+    def zero_grad(self, set_to_none: bool = True):
+        """set_to_none=False zeroes the flat gradient buffer with one memset."""
+        if not set_to_none and self._flat is not None:
+            self._flat["buf"].zero_()
+            for p in self.parameters():
+                if p.grad is not None and not (self._flat["buf"].data_ptr() <= p.grad.data_ptr() <
+                                               self._flat["buf"].data_ptr() + 4 * self._flat["buf"].numel()):
+                    p.grad.zero_()
+            return
+        super().zero_grad(set_to_none=set_to_none)
+
     def _autograd_anchor(self):
         dev = next(self.parameters()).device
         if self._anchor is None or self._anchor.device != dev:
