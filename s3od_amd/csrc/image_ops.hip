@@ -1,0 +1,134 @@
+// remove_background pre/post-processing on device (src/s3od/predictor.py:79-139, src/s3od/utils.py).
+//   preprocess: uint8 HWC image -> letterbox resize (cv2.resize INTER_LINEAR fixed-point, SIMD-path
+//               rounding) into a zero-padded S x S canvas -> (x/255 - mean)/std (float64 math,
+//               rounded to fp32 like numpy) -> fp32 NCHW [1,3,S,S]
+//   postprocess: sigmoid -> unpad -> antialiased bilinear resize to the original size
+//               (F.interpolate(..., antialias=True), separable triangle filter, horizontal first)
+#include "common.hpp"
+
+namespace {
+constexpr int COEF_BITS = 11, COEF_SCALE = 1 << COEF_BITS;
+
+// cv2 resizeGeneric_ coefficient for one destination index (INTER_LINEAR, fixed point)
+DEV void cv_coef(int d, int ssize, int dsize, int& s0, int& s1, int& a0, int& a1) {
+  double scale = (double)ssize / (double)dsize;
+  float f = (float)((d + 0.5) * scale - 0.5);
+  int s = (int)floorf(f);
+  f -= (float)s;
+  if (s < 0) { f = 0.f; s = 0; }
+  if (s >= ssize - 1) { f = 0.f; s = ssize - 1; }
+  s0 = s; s1 = min(s + 1, ssize - 1);
+  int c0 = (int)rintf((1.f - f) * COEF_SCALE);      // saturate_cast<short>(float) rounds to nearest
+  int c1 = (int)rintf(f * COEF_SCALE);
+  a0 = c0; a1 = c1;
+}
+}  // namespace
+
+// one thread per destination pixel of the resized (new_h x new_w) image; writes normalised fp32
+// into the S x S canvas at (pad_h + y, pad_w + x).  The canvas must be pre-filled with the
+// normalised value of a zero pixel (kernel below).
+__global__ void preprocess_kernel(const unsigned char* __restrict__ img, int H0, int W0, int new_h, int new_w,
+                                  int pad_h, int pad_w, int S, float* __restrict__ out) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= new_w || y >= new_h) return;
+  const double mean[3] = {0.485, 0.456, 0.406}, stdv[3] = {0.229, 0.224, 0.225};
+  int v[3];
+  if (new_h == H0 && new_w == W0) {
+    for (int c = 0; c < 3; c++) v[c] = img[((long)y * W0 + x) * 3 + c];
+  } else {
+    int sx0, sx1, ax0, ax1, sy0, sy1, by0, by1;
+    cv_coef(x, W0, new_w, sx0, sx1, ax0, ax1);
+    cv_coef(y, H0, new_h, sy0, sy1, by0, by1);
+    for (int c = 0; c < 3; c++) {
+      int r0 = img[((long)sy0 * W0 + sx0) * 3 + c] * ax0 + img[((long)sy0 * W0 + sx1) * 3 + c] * ax1;
+      int r1 = img[((long)sy1 * W0 + sx0) * 3 + c] * ax0 + img[((long)sy1 * W0 + sx1) * 3 + c] * ax1;
+      // VResizeLinearVec_32s8u: sat_u8((mulhi16(r0>>4, b0) + mulhi16(r1>>4, b1) + 2) >> 2)
+      int t0 = ((short)(r0 >> 4) * (short)by0) >> 16;
+      int t1 = ((short)(r1 >> 4) * (short)by1) >> 16;
+      int o = (t0 + t1 + 2) >> 2;
+      v[c] = o < 0 ? 0 : (o > 255 ? 255 : o);
+    }
+  }
+  for (int c = 0; c < 3; c++) {
+    float t = (float)v[c] / 255.0f;                  // float32 / python float -> float32 (numpy 2)
+    double d = ((double)t - mean[c]) / stdv[c];       // - float64 mean, / float64 std
+    out[((long)c * S + (pad_h + y)) * S + (pad_w + x)] = (float)d;
+  }
+}
+
+__global__ void canvas_fill_kernel(float* out, int S) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 3L * S * S) return;
+  int c = i / ((long)S * S);
+  const double mean[3] = {0.485, 0.456, 0.406}, stdv[3] = {0.229, 0.224, 0.225};
+  out[i] = (float)((0.0 - mean[c]) / stdv[c]);
+}
+
+// ---------------------------------------------------------------- antialiased bilinear
+// PyTorch _upsample_bilinear2d_aa weights for output index i (align_corners=False)
+DEV int aa_weights(int i, int in, int out, float* w, int maxw) {
+  float scale = (float)in / (float)out;
+  float support = scale >= 1.f ? scale : 1.f;
+  float center = scale * (i + 0.5f);
+  float invscale = scale >= 1.f ? 1.f / scale : 1.f;
+  int xmin = max((int)(center - support + 0.5f), 0);
+  int xsize = min((int)(center + support + 0.5f), in) - xmin;
+  if (xsize > maxw) xsize = maxw;
+  float tot = 0.f;
+  for (int j = 0; j < xsize; j++) {
+    float x = (j + xmin - center + 0.5f) * invscale;
+    float ww = fabsf(x) < 1.f ? 1.f - fabsf(x) : 0.f;
+    w[j] = ww; tot += ww;
+  }
+  for (int j = 0; j < xsize; j++) w[j] = tot != 0.f ? w[j] / tot : 0.f;
+  return xmin | (xsize << 20);
+}
+
+// pass 1: sigmoid + crop + horizontal resample: [3][S][S] logits -> tmp [3][h][W0]
+__global__ void post_h_kernel(const float* __restrict__ logits, int S, int pad_h, int pad_w, int h, int w, int W0, float* __restrict__ tmp) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, c = blockIdx.z;
+  if (x >= W0) return;
+  float wt[64];
+  int r = aa_weights(x, w, W0, wt, 64);
+  int xmin = r & 0xFFFFF, xs = r >> 20;
+  const float* row = logits + ((long)c * S + (pad_h + y)) * S + pad_w;
+  float acc = 0.f;
+  for (int j = 0; j < xs; j++) acc += wt[j] * (1.f / (1.f + expf(-row[xmin + j])));
+  tmp[((long)c * h + y) * W0 + x] = acc;
+}
+
+// pass 2: vertical resample -> out [3][H0][W0]
+__global__ void post_v_kernel(const float* __restrict__ tmp, int h, int H0, int W0, float* __restrict__ out) {
+  int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, c = blockIdx.z;
+  if (x >= W0) return;
+  float wt[64];
+  int r = aa_weights(y, h, H0, wt, 64);
+  int ymin = r & 0xFFFFF, ys = r >> 20;
+  float acc = 0.f;
+  for (int j = 0; j < ys; j++) acc += wt[j] * tmp[((long)c * h + ymin + j) * W0 + x];
+  out[((long)c * H0 + y) * W0 + x] = acc;
+}
+
+extern "C" {
+
+// img: device uint8 [H0][W0][3]; out: fp32 [1][3][S][S]
+int s3od_preprocess(const void* img, int H0, int W0, int new_h, int new_w, int pad_h, int pad_w, int S, float* out, void* stream) {
+  S3OD_REQUIRE(new_h + pad_h <= S && new_w + pad_w <= S, "preprocess: resized image does not fit the canvas");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(canvas_fill_kernel, dim3(cdiv(3L * S * S, 256)), dim3(256), 0, st, out, S);
+  hipLaunchKernelGGL(preprocess_kernel, dim3(cdiv(new_w, 256), new_h), dim3(256), 0, st, (const unsigned char*)img, H0, W0,
+                     new_h, new_w, pad_h, pad_w, S, out);
+  return s3od_check_launch("preprocess");
+}
+
+// logits: fp32 [3][S][S] (one image); tmp: fp32 [3][h][W0]; out: fp32 [3][H0][W0]
+int s3od_sigmoid_unpad_resize(const float* logits, int S, int pad_h, int pad_w, int h, int w, int H0, int W0,
+                              float* tmp, float* out, void* stream) {
+  S3OD_REQUIRE((float)w / W0 < 32.f && (float)h / H0 < 32.f, "postprocess: downscale factor too large");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(post_h_kernel, dim3(cdiv(W0, 256), h, 3), dim3(256), 0, st, logits, S, pad_h, pad_w, h, w, W0, tmp);
+  hipLaunchKernelGGL(post_v_kernel, dim3(cdiv(W0, 256), H0, 3), dim3(256), 0, st, tmp, h, H0, W0, out);
+  return s3od_check_launch("sigmoid_unpad_resize");
+}
+
+}  // extern "C"

@@ -28,7 +28,10 @@ def _container():
 
 
 class _Tree(nn.Module):
-    pass
+    """Plain container; numeric children are indexable like the reference's ModuleList/Sequential."""
+
+    def __getitem__(self, i):
+        return self._modules[str(i)]
 
 
 def _build_tree(root: nn.Module, specs):
