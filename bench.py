@@ -89,6 +89,20 @@ def cpu_baseline(S, mode, threads):
                                       f"fp32 oracle (oracle/s3od_oracle.py), {n} timed iter after 1 warm-up, {threads} threads"}
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/<tag>_pmc.json, written by tools/collect_profiles.py), or None."""
+    files = sorted((ROOT / "profiles").glob("*_pmc.json"))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("kernel") == kernel:
+            return {"bytes": d["traffic_bytes_per_launch"], "source": f"profiles/{f.name}"}
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -177,6 +191,7 @@ def main():
         unit = "images/s" if args.mode == "train" else "masks/s"
         peak = PEAK_BF16 if args.dtype == "bf16" else PEAK_F32
         achieved = attn_flops(B, S) / (kms * 1e-3) if kms > 0 else 0.0
+        tr = pmc_traffic("attn_fwd_kernel") if (B == 16 and S == 1024 and args.dtype == "bf16") else None
         res = {
             "metric": metric, "value": round(value, 3), "unit": unit, "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
@@ -188,7 +203,9 @@ def main():
                        "image_size": S, "parallelism": f"dp{world}"},
             "roofline": {"kernel": "attn_fwd_kernel (flash attention fwd, 1 launch per ViT layer)", "bound": "mfma",
                          "achieved": round(achieved / 1e12, 2), "peak": round(peak / 1e12, 1), "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4), "traffic": None,
+                         "frac": round(achieved / peak, 4), "traffic": round(tr["bytes"]) if tr else None,
+                         "traffic_unit": "bytes/launch (FETCH_SIZE*2 + WRITE_SIZE, gfx950-corrected)",
+                         "traffic_source": tr["source"] if tr else None,
                          "flops_per_launch": attn_flops(B, S), "mean_launch_ms": round(kms, 4), "launches": len(ev)},
             "finite": ok,
         }
