@@ -1,6 +1,8 @@
 // Flash attention for DINOv3 ViT-B/16 (12 heads x d=64, non-causal, no mask), gfx950.
 // Reference semantics: SDPA softmax(q k^T / 8) v (tf:integrations/sdpa_attention.py:79-166,
-// tf:models/dinov3_vit/modeling_dinov3_vit.py:294-334).  q arrives pre-scaled by 1/8.
+// tf:models/dinov3_vit/modeling_dinov3_vit.py:294-334).
+// Conventions (base-2 domain): q arrives pre-scaled by log2(e)/8 (S3OD_QSCALE, applied in the QKV
+// epilogue), so q.k is the score in log2 units; LSE is stored in log2 units (lse2 = m + log2 l).
 //
 // Forward: one workgroup = 4 waves = 128 query rows of one (b, h); each wave owns 32 queries.
 // "Swapped" products keep the softmax row lane-local:
@@ -8,8 +10,14 @@
 //   O^T[d][q]  += V^T . P^T     (A = V^T via ds_read_b64_tr_b16, B = P^T straight from the
 //                                S^T accumulator registers; the K-order of the MFMA is permuted
 //                                identically on both operands, so no shuffles / LDS round trip)
+// The loop is VALU-issue bound on CDNA4 (an MFMA 16x16x32 leaves room for ~2 VALU ops), so the
+// bf16 path spends as little VALU per score as possible:
+//   * the running row max m is folded into the S accumulator's C operand (C = -m), so
+//     P = exp2(acc) is ONE v_exp per score;
+//   * lazy rescaling: m only moves when some score exceeds it by > 2^8 (wave-uniform branch);
+//   * the row sum l comes out of the matrix core: l += 1^T P^T (one extra MFMA per 32 keys).
 // K/V tiles of 64 keys are register-staged into double-buffered LDS (one barrier per tile).
-// T=float runs the same dataflow on v_mfma_f32_16x16x4_f32 (strict-parity path).
+// T=float runs the exact online softmax on v_mfma_f32_16x16x4_f32 (strict-parity path).
 #include "common.hpp"
 #include <type_traits>
 
@@ -21,7 +29,10 @@
   } while (0)
 
 namespace {
-constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+constexpr float RESCALE_TH = 8.f;       // lazy-rescale threshold (log2 units): P <= 2^8 between rescales
+
+DEV float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }   // bare v_exp_f32 (no denormal fix-up)
 
 // LDS images of a 64-key x 64-d tile.  bf16: 128-B rows, 32-B slots XOR (key>>1)&3 (tr reads),
 // 16-B slots XOR ((key>>1)&7) for row (ds_read_b128) reads.  f32: 256-B rows + 16-B pad.
@@ -62,6 +73,16 @@ template <typename T> struct Stage {
     }
   }
 };
+
+DEV float max16(const f32x4* s) {   // max over 4 accumulators (16 values)
+  float a = fmaxf(fmaxf(s[0][0], s[0][1]), s[0][2]);
+  a = fmaxf(fmaxf(a, s[0][3]), s[1][0]); a = fmaxf(fmaxf(a, s[1][1]), s[1][2]);
+  a = fmaxf(fmaxf(a, s[1][3]), s[2][0]); a = fmaxf(fmaxf(a, s[2][1]), s[2][2]);
+  a = fmaxf(fmaxf(a, s[2][3]), s[3][0]); a = fmaxf(fmaxf(a, s[3][1]), s[3][2]);
+  return fmaxf(a, s[3][3]);
+}
+DEV float xmax4(float v) { v = fmaxf(v, __shfl_xor(v, 16)); return fmaxf(v, __shfl_xor(v, 32)); }
+DEV float xsum4(float v) { v += __shfl_xor(v, 16); return v + __shfl_xor(v, 32); }
 }  // namespace
 
 template <typename T>
@@ -96,7 +117,10 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const T* __restrict__ Q, 
   f32x4 o[4][2];
 #pragma unroll
   for (int i = 0; i < 4; i++) { o[i][0] = f32x4{0, 0, 0, 0}; o[i][1] = f32x4{0, 0, 0, 0}; }
+  // running max m (log2 units); bf16: C operand -m of the S MFMA, row sums in lacc (MFMA)
   float mrow[2] = {-INFINITY, -INFINITY}, lrow[2] = {0.f, 0.f};
+  f32x4 negm[2] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
+  f32x4 lacc[2] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
 
   Stage<T> stg;
   const int nkt = (N + 63) / 64;
@@ -109,22 +133,25 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const T* __restrict__ Q, 
     if (more) stg.load(Kp, Vp, (kt + 1) * 64, N, tid);
     const char* ks = smem + cur * 2 * L::BYTES;
     const char* vs = ks + L::BYTES;
-    // ---- S^T = K Q^T : acc[ks][qs], element i: key = ks*16 + 4g + i, query = qs*16 + li
+    // ---- S^T = K Q^T (- m) : acc[kb][qs], element i: key = kb*16 + 4g + i, query = qs*16 + li
     f32x4 s[4][2];
 #pragma unroll
     for (int kb = 0; kb < 4; kb++) {
-      s[kb][0] = f32x4{0, 0, 0, 0}; s[kb][1] = f32x4{0, 0, 0, 0};
+      if constexpr (F32) {
+        s[kb][0] = f32x4{0, 0, 0, 0}; s[kb][1] = f32x4{0, 0, 0, 0};
 #pragma unroll
-      for (int kk = 0; kk < QK; kk++) {
-        if constexpr (F32) {
+        for (int kk = 0; kk < QK; kk++) {
           float a = *(const float*)(ks + L::krow(kb * 16 + li, (kk * 4 + g) * 4));
           s[kb][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, qf[0][kk], s[kb][0], 0, 0, 0);
           s[kb][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, qf[1][kk], s[kb][1], 0, 0, 0);
-        } else {
-          bf16x8 a = *(const bf16x8*)(ks + L::krow(kb * 16 + li, kk * 64 + g * 16));
-          s[kb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[0][kk], s[kb][0], 0, 0, 0);
-          s[kb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[1][kk], s[kb][1], 0, 0, 0);
         }
+      } else {
+        bf16x8 a0 = *(const bf16x8*)(ks + L::krow(kb * 16 + li, g * 16));
+        bf16x8 a1 = *(const bf16x8*)(ks + L::krow(kb * 16 + li, 64 + g * 16));
+        s[kb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, qf[0][0], negm[0], 0, 0, 0);
+        s[kb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, qf[1][0], negm[1], 0, 0, 0);
+        s[kb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, qf[0][1], s[kb][0], 0, 0, 0);
+        s[kb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, qf[1][1], s[kb][1], 0, 0, 0);
       }
     }
     // ---- mask keys >= N (last tile only)
@@ -137,33 +164,24 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const T* __restrict__ Q, 
           if (key >= N) { s[kb][0][i] = -INFINITY; s[kb][1][i] = -INFINITY; }
         }
     }
-    // ---- online softmax per query column
-#pragma unroll
-    for (int qs = 0; qs < 2; qs++) {
-      float mx = -INFINITY;
-#pragma unroll
-      for (int kb = 0; kb < 4; kb++)
-#pragma unroll
-        for (int i = 0; i < 4; i++) mx = fmaxf(mx, s[kb][qs][i]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16));
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      float mnew = fmaxf(mrow[qs], mx);
-      float alpha = exp2f((mrow[qs] - mnew) * LOG2E);
-      float nb = mnew * LOG2E;
-      float sum = 0.f;
-#pragma unroll
-      for (int kb = 0; kb < 4; kb++)
-#pragma unroll
-        for (int i = 0; i < 4; i++) { float p = exp2f(s[kb][qs][i] * LOG2E - nb); s[kb][qs][i] = p; sum += p; }
-      sum += __shfl_xor(sum, 16);
-      sum += __shfl_xor(sum, 32);
-      lrow[qs] = lrow[qs] * alpha + sum;
-      mrow[qs] = mnew;
-#pragma unroll
-      for (int ds = 0; ds < 4; ds++) o[ds][qs] *= alpha;
-    }
-    // ---- O^T += V^T P^T
     if constexpr (F32) {
+      // ---- exact online softmax per query column
+#pragma unroll
+      for (int qs = 0; qs < 2; qs++) {
+        f32x4 col[4] = {s[0][qs], s[1][qs], s[2][qs], s[3][qs]};
+        float mx = xmax4(max16(col));
+        float mnew = fmaxf(mrow[qs], mx);
+        float alpha = fexp2(mrow[qs] - mnew);
+        float sum = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 4; kb++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) { float p = fexp2(s[kb][qs][i] - mnew); s[kb][qs][i] = p; sum += p; }
+        lrow[qs] = lrow[qs] * alpha + xsum4(sum);
+        mrow[qs] = mnew;
+#pragma unroll
+        for (int ds = 0; ds < 4; ds++) o[ds][qs] *= alpha;
+      }
 #pragma unroll
       for (int kb = 0; kb < 4; kb++)
 #pragma unroll
@@ -177,14 +195,41 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const T* __restrict__ Q, 
           }
         }
     } else {
+      // ---- lazy max: s already holds score - m.  The first tile sets m exactly; later tiles only
+      // rescale when a score exceeds m by more than RESCALE_TH (wave-uniform branch).
+      f32x4 c0[4] = {s[0][0], s[1][0], s[2][0], s[3][0]}, c1[4] = {s[0][1], s[1][1], s[2][1], s[3][1]};
+      float lm0 = max16(c0), lm1 = max16(c1);
+      if (kt == 0 || __any(fmaxf(lm0, lm1) > RESCALE_TH)) {
+        float lmq[2] = {lm0, lm1};
+#pragma unroll
+        for (int qs = 0; qs < 2; qs++) {
+          float d = xmax4(lmq[qs]);
+          d = kt == 0 ? d : fmaxf(d, 0.f);
+          mrow[qs] = kt == 0 ? d : mrow[qs] + d;
+          float alpha = kt == 0 ? 1.f : fexp2(-d);
+#pragma unroll
+          for (int kb = 0; kb < 4; kb++) s[kb][qs] -= d;
+#pragma unroll
+          for (int ds = 0; ds < 4; ds++) o[ds][qs] *= alpha;
+          lacc[qs] *= alpha;
+          negm[qs] = f32x4{-mrow[qs], -mrow[qs], -mrow[qs], -mrow[qs]};
+        }
+      }
+      // ---- P = exp2(s); O^T += V^T P^T ; l += 1^T P^T
       typedef __attribute__((address_space(3))) s16x4 lds_s4;
+      bf16x8 ones;
+#pragma unroll
+      for (int e = 0; e < 8; e++) ones[e] = (bf16)1.f;
 #pragma unroll
       for (int kst = 0; kst < 2; kst++) {
         bf16x8 pb[2];
 #pragma unroll
         for (int qs = 0; qs < 2; qs++)
 #pragma unroll
-          for (int i = 0; i < 4; i++) { pb[qs][i] = (bf16)s[2 * kst][qs][i]; pb[qs][4 + i] = (bf16)s[2 * kst + 1][qs][i]; }
+          for (int i = 0; i < 4; i++) {
+            pb[qs][i] = (bf16)fexp2(s[2 * kst][qs][i]);
+            pb[qs][4 + i] = (bf16)fexp2(s[2 * kst + 1][qs][i]);
+          }
         const int q = li >> 2, p = li & 3;
 #pragma unroll
         for (int ds = 0; ds < 4; ds++) {
@@ -196,13 +241,16 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const T* __restrict__ Q, 
           o[ds][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb[0], o[ds][0], 0, 0, 0);
           o[ds][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb[1], o[ds][1], 0, 0, 0);
         }
+        lacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[0], lacc[0], 0, 0, 0);
+        lacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[1], lacc[1], 0, 0, 0);
       }
     }
     if (more) stg.store(smem + (cur ^ 1) * 2 * L::BYTES, smem + (cur ^ 1) * 2 * L::BYTES + L::BYTES, tid);
     __syncthreads();
     cur ^= 1;
   }
-  // ---- epilogue: O[b][t][h*64 + d], d = ds*16 + 4g + i ; LSE = m + ln(l)
+  if constexpr (!F32) { lrow[0] = lacc[0][0]; lrow[1] = lacc[1][0]; }
+  // ---- epilogue: O[b][t][h*64 + d], d = ds*16 + 4g + i ; LSE (log2 units) = m + log2(l)
 #pragma unroll
   for (int qs = 0; qs < 2; qs++) {
     int q = q0 + qs * 16 + li;
@@ -215,7 +263,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const T* __restrict__ Q, 
       if constexpr (F32) *(float4*)(orow + d) = make_float4(o[ds][qs][0] * inv, o[ds][qs][1] * inv, o[ds][qs][2] * inv, o[ds][qs][3] * inv);
       else { bf16x4 v = {(bf16)(o[ds][qs][0] * inv), (bf16)(o[ds][qs][1] * inv), (bf16)(o[ds][qs][2] * inv), (bf16)(o[ds][qs][3] * inv)}; *(bf16x4*)(orow + d) = v; }
     }
-    if (g == 0 && LSE) LSE[(long)bh * N + q] = mrow[qs] + logf(lrow[qs]);
+    if (g == 0 && LSE) LSE[(long)bh * N + q] = mrow[qs] + __log2f(lrow[qs]);
   }
 }
 
@@ -345,7 +393,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const T* __restrict_
   auto stage_load = [&](int qt) {
     tq.load(Qp, 64, qt * 64, N, tid);
     tdo.load(dOp, ldo, qt * 64, N, tid);
-    if (tid < 64) { int q = qt * 64 + tid; lse_r = q < N ? Lp[q] : INFINITY; dl_r = q < N ? Dp[q] : 0.f; }
+    if (tid < 64) { int q = qt * 64 + tid; lse_r = q < N ? -Lp[q] : -INFINITY; dl_r = q < N ? -Dp[q] : 0.f; }   // negated
   };
   auto stage_store = [&](char* base) {
     tq.store(base, tid); tdo.store(base + I::BYTES, tid);
@@ -363,11 +411,15 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const T* __restrict_
     const char* dos = qs_ + I::BYTES;
     const float* lsel = (const float*)(qs_ + 2 * I::BYTES);
     const float* dll = lsel + 64;
+    // accumulators start at -LSE[q] / -delta[q] (q = qb*16 + 4g + i), so after the MFMAs
+    // s = score - lse (log2 units) and dp = dO.v - delta
     f32x4 s[4][2], dp[4][2];
 #pragma unroll
-    for (int qb = 0; qb < 4; qb++)
+    for (int qb = 0; qb < 4; qb++) {
+      f32x4 nl = *(const f32x4*)(lsel + qb * 16 + 4 * g), nd = *(const f32x4*)(dll + qb * 16 + 4 * g);
 #pragma unroll
-      for (int ks = 0; ks < 2; ks++) { s[qb][ks] = f32x4{0, 0, 0, 0}; dp[qb][ks] = f32x4{0, 0, 0, 0}; }
+      for (int ks = 0; ks < 2; ks++) { s[qb][ks] = nl; dp[qb][ks] = nd; }
+    }
 #pragma unroll
     for (int qb = 0; qb < 4; qb++) {
 #pragma unroll
@@ -383,20 +435,17 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const T* __restrict_
         }
       }
     }
-    // P = exp(S - LSE[q]), dS = P*(dP - delta[q]);  q = qb*16 + 4g + i
+    // P = exp2(S - LSE[q]), dS = P*(dP - delta[q])   (invalid q: LSE = +inf -> P = 0)
 #pragma unroll
     for (int qb = 0; qb < 4; qb++)
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        int qq = qb * 16 + 4 * g + i;
-        float L = lsel[qq], Dv = dll[qq];
+      for (int ks = 0; ks < 2; ks++)
 #pragma unroll
-        for (int ks = 0; ks < 2; ks++) {
-          float p = __expf(s[qb][ks][i] - L);
+        for (int i = 0; i < 4; i++) {
+          float p = fexp2(s[qb][ks][i]);
           s[qb][ks][i] = p;
-          dp[qb][ks][i] = p * (dp[qb][ks][i] - Dv);
+          dp[qb][ks][i] = p * dp[qb][ks][i];
         }
-      }
     // dV^T += dO^T P ; dK^T += Q^T dS
     if constexpr (F32) {
 #pragma unroll
@@ -439,6 +488,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const T* __restrict_
 #pragma unroll
     for (int ds = 0; ds < 4; ds++) {
       int d = ds * 16 + 4 * g;
+      dk[ds][ks] *= LN2;   // d(q.k*ln2)/dk with q in log2 scaling
       if constexpr (F32) {
         *(float4*)(dkr + d) = make_float4(dk[ds][ks][0], dk[ds][ks][1], dk[ds][ks][2], dk[ds][ks][3]);
         *(float4*)(dvr + d) = make_float4(dv[ds][ks][0], dv[ds][ks][1], dv[ds][ks][2], dv[ds][ks][3]);
@@ -492,6 +542,9 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const T* __restrict__ 
   f32x4 dq[4][2];
 #pragma unroll
   for (int i = 0; i < 4; i++) { dq[i][0] = f32x4{0, 0, 0, 0}; dq[i][1] = f32x4{0, 0, 0, 0}; }
+  f32x4 nl[2], nd[2];   // C operands: -lse (log2 units), -delta of the lane's query column
+#pragma unroll
+  for (int qs = 0; qs < 2; qs++) { nl[qs] = f32x4{-Lq[qs], -Lq[qs], -Lq[qs], -Lq[qs]}; nd[qs] = f32x4{-Dq[qs], -Dq[qs], -Dq[qs], -Dq[qs]}; }
   RowTile<T> tk, tv;
   const int nkt = (N + 63) / 64;
   tk.load(Kp, 64, 0, N, tid); tv.load(Vp, 64, 0, N, tid);
@@ -506,7 +559,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const T* __restrict__ 
     f32x4 s[4][2], dp[4][2];
 #pragma unroll
     for (int kb = 0; kb < 4; kb++) {
-      s[kb][0] = s[kb][1] = dp[kb][0] = dp[kb][1] = f32x4{0, 0, 0, 0};
+      s[kb][0] = nl[0]; s[kb][1] = nl[1]; dp[kb][0] = nd[0]; dp[kb][1] = nd[1];
 #pragma unroll
       for (int kk = 0; kk < KK; kk++) {
         if constexpr (F32) {
@@ -520,17 +573,20 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const T* __restrict__ 
         }
       }
     }
+    // dS^T = exp2(s - lse) * (dp - delta)
 #pragma unroll
     for (int kb = 0; kb < 4; kb++)
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        bool valid = kt * 64 + kb * 16 + 4 * g + i < N;
+      for (int qs = 0; qs < 2; qs++)
 #pragma unroll
-        for (int qs = 0; qs < 2; qs++) {
-          float p = valid ? __expf(s[kb][qs][i] - Lq[qs]) : 0.f;
-          dp[kb][qs][i] = p * (dp[kb][qs][i] - Dq[qs]);
-        }
-      }
+        for (int i = 0; i < 4; i++) dp[kb][qs][i] *= fexp2(s[kb][qs][i]);
+    if (kt * 64 + 64 > N) {   // last tile: zero dS of keys >= N (exp2(-lse) may overflow)
+#pragma unroll
+      for (int kb = 0; kb < 4; kb++)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          if (kt * 64 + kb * 16 + 4 * g + i >= N) { dp[kb][0][i] = 0.f; dp[kb][1][i] = 0.f; }
+    }
     if constexpr (F32) {
 #pragma unroll
       for (int kb = 0; kb < 4; kb++)
@@ -576,7 +632,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const T* __restrict__ 
 
 extern "C" {
 
-// q,k,v: [B*H, N, 64] (q pre-scaled by 1/8); o: [B, N, H*64]; lse: [B*H, N] fp32 (optional)
+// q,k,v: [B*H, N, 64] (q pre-scaled by log2(e)/8); o: [B, N, H*64]; lse: [B*H, N] fp32, log2 units (optional)
 int s3od_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int N, void* stream) {
   dim3 grid(cdiv(N, 128), B * H);
   DISPATCH_T(dtype, {
@@ -587,7 +643,7 @@ int s3od_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* 
 
 
 // backward: o, do: [B, N, H*64]; q,k,v: [B*H, N, 64]; lse, delta(workspace): [B*H, N] fp32
-// outputs dq (w.r.t. the 1/8-scaled q), dk, dv: [B*H, N, 64]
+// outputs dq = dS.K (dS in natural units; the caller scales by 1/8 for d(rope(q))), dk, dv: [B*H, N, 64]
 int s3od_attn_bwd(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
                   float* delta, void* dq, void* dk, void* dv, int B, int H, int N, void* stream) {
   hipStream_t st = (hipStream_t)stream;

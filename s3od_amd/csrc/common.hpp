@@ -15,6 +15,11 @@ enum { S3OD_F32 = 0, S3OD_BF16 = 1 };
 
 #define DEV __device__ __forceinline__
 
+// q is stored pre-scaled by log2(e)/sqrt(64) so attention scores come out in log2 units
+// (attention.hip); the q-gradient path (qkv_unrope) still scales by 1/8 because the attention
+// backward returns dS.K with dS in natural units (see attention.hip).
+constexpr float S3OD_QSCALE = 0.125f * 1.4426950408889634f;
+
 // ------------------------------------------------------------------ error reporting
 void s3od_set_error(const char* fmt, ...);
 int s3od_check_launch(const char* what);

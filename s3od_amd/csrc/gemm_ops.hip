@@ -62,7 +62,7 @@ template <typename T> struct EpiQKV {
       }
       if (which == 0) {
 #pragma unroll
-        for (int e = 0; e < 8; e++) val[e] *= 0.125f;
+        for (int e = 0; e < 8; e++) val[e] *= S3OD_QSCALE;
       }
       T* dst = which == 0 ? q : (which == 1 ? k : v);
       store8<T>(dst + (((long)b * H + h) * Ntok + t) * 64 + d0, val);

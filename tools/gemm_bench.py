@@ -72,7 +72,25 @@ def attn(B, N):
     print(f"attn fwd B={B} N={N}: {t * 1e6:8.1f} us  {4 * B * 12 * N * N * 64 / t / 1e12:7.1f} TF/s")
 
 
+def attn_bwd(B, N):
+    q = torch.randn(B * 12, N, 64, device="cuda").bfloat16() * 0.3
+    k, v = torch.randn_like(q), torch.randn_like(q)
+    o = torch.empty(B, N, 768, device="cuda", dtype=torch.bfloat16)
+    lse = torch.empty(B * 12, N, device="cuda")
+    lib()("s3od_attn_fwd", BF16, q, k, v, o, lse, B, 12, N, stream())
+    do = torch.randn_like(o)
+    delta = torch.empty_like(lse)
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(q), torch.empty_like(q)
+    f = lambda: lib()("s3od_attn_bwd", BF16, q, k, v, o, do, lse, delta, dq, dk, dv, B, 12, N, stream())
+    t = timeit(f, 10)
+    print(f"attn bwd B={B} N={N}: {t * 1e6:8.1f} us  {10 * B * 12 * N * N * 64 / t / 1e12:7.1f} TF/s (5 GEMMs; 4 algorithmic)")
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "attn":
+        attn(16, 4101)
+        attn_bwd(16, 4101)
+        sys.exit(0)
     M = 16 * 4101
     lin(4096, 4096, 4096)
     lin(M, 2304, 768)
