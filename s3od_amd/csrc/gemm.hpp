@@ -87,21 +87,32 @@ template <typename T> DEV uint4 relu16(uint4 v) {
 }
 
 // ------------------------------------------------------------------ operand loaders
-// Global -> LDS by LDS-DMA (global_load_lds_dwordx4): one wave instruction writes 1 KiB of LDS
-// lane-linearly (wave base + lane*16), so the XOR swizzles are applied to the per-lane SOURCE
-// address (guide §5.4 rule 21).  Out-of-range chunks (padding, tails) read a zero page.
+// Global -> LDS by LDS-DMA through a buffer resource (buffer_load_dwordx4 ... lds): one wave
+// instruction writes 1 KiB of LDS lane-linearly (M0 = wave base, + lane*16), so the XOR
+// swizzles are applied to the per-lane SOURCE offset (guide §5.4 rule 21).
+//   * the descriptor (base, byte size) is built from kernel arguments only -> SGPRs;
+//   * each lane keeps a 32-bit byte offset that is advanced by a uniform step per K tile, so the
+//     steady-state address cost is ~1 VALU per load (no 64-bit pointer math);
+//   * out-of-range chunks (padding taps, row/column tails) use an offset beyond the descriptor's
+//     size: the hardware range check returns zeros (no zero page, no per-load select);
+//   * the wave index is readfirstlane'd so every M0 value is computed on the scalar unit.
 // A tile of R rows is R*128 bytes: NIW = R*128/1024/GEMM_WAVES = R/64 instructions per wave.
 //   KC image: instruction slot o = (wave*NIW + i)*1024 + lane*16 -> row o>>7, physical 16-B slot
 //             (o>>4)&7, logical chunk = phys ^ ((row>>1)&7)
 //   MC image: k-row o / RB, physical byte o % RB, logical 32-B slot = phys32 ^ g(k)
-__device__ __attribute__((aligned(16))) uint4 g_s3od_zero[8];
+// Operands must be < 3.75 GiB (checked on the host by buf_ok()).
+constexpr unsigned long BUF_MAX = 0xF0000000ul;
+constexpr unsigned BUF_OOB = 0xF8000000u;      // any offset >= BUF_MAX reads zeros
 
 typedef __attribute__((address_space(3))) void lds_void;
-typedef __attribute__((address_space(1))) void glob_void;
-DEV void glds16(const void* src, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((glob_void*)src, (lds_void*)lds_wave_base, 16, 0, 0);
+DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* p, unsigned long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(unsigned)(bytes < BUF_MAX ? bytes : BUF_MAX), 0x00020000);
 }
-DEV const void* zero_src() { return (const void*)g_s3od_zero; }
+DEV void blds16(__amdgpu_buffer_rsrc_t r, unsigned voff, char* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_wave_base, 16, voff, 0, 0, 0);
+}
+DEV int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+#define HD __host__ __device__
 
 template <int RB> DEV int mc_logical_byte(int k, int phys) {
   constexpr int SLOTS = RB / 32;
@@ -129,25 +140,29 @@ template <typename T, int R> struct DenseKC {          // X[row*ld + k]
   static constexpr bool KCL = true, RELU = false;
   typedef KCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* p; long ld; int nrows, K; int relu;
-  const T* rowp[NIW]; int kel[NIW]; bool rv[NIW];
+  unsigned vo[NIW]; int kel[NIW];
+  HD unsigned long bytes() const { return ((unsigned long)(nrows - 1) * ld + K) * sizeof(T); }
+  HD bool buf_ok() const { return bytes() < BUF_MAX && (unsigned long)K * sizeof(T) < 0x4000000ul; }
   DEV void setup(int t0, int tid) {
-    const int lane = tid & 63, wave = tid >> 6;
+    const int lane = tid & 63, wave = wave_id();
 #pragma unroll
     for (int i = 0; i < NIW; i++) {
       int r = t0 + G::row(wave, i, lane);
-      rv[i] = r < nrows;
-      rowp[i] = p + (long)(rv[i] ? r : 0) * ld;
       kel[i] = G::kel(wave, i, lane);
+      vo[i] = r < nrows ? (unsigned)(((long)r * ld + kel[i]) * sizeof(T)) : BUF_OOB;
     }
   }
   DEV void issue(int kt, char* tile) {
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_id();
+    const auto rs = make_rsrc(p, bytes());
+    const unsigned adv = (unsigned)(kt * BK * sizeof(T));
+    if ((kt + 1) * BK > K) {          // K tail (uniform branch)
 #pragma unroll
-    for (int i = 0; i < NIW; i++) {
-      int k = kt * BK + kel[i];
-      const void* src = (rv[i] && k < K) ? (const void*)(rowp[i] + k) : zero_src();
-      glds16(src, tile + (wave * NIW + i) * 1024);
+      for (int i = 0; i < NIW; i++) blds16(rs, kt * BK + kel[i] < K ? vo[i] + adv : BUF_OOB, tile + (wave * NIW + i) * 1024);
+      return;
     }
+#pragma unroll
+    for (int i = 0; i < NIW; i++) blds16(rs, vo[i] + adv, tile + (wave * NIW + i) * 1024);
   }
 };
 
@@ -156,21 +171,57 @@ template <typename T, int R> struct DenseMC {          // X[k*ld + col]
   typedef MCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* p; long ld; int K, ncols;
   int relu = 0;
-  int kr[NIW], cl[NIW];
+  unsigned vo[NIW]; int kr[NIW]; bool cv[NIW];
+  HD unsigned long bytes() const { return ((unsigned long)(K - 1) * ld + ncols) * sizeof(T); }
+  HD bool buf_ok() const { return bytes() < BUF_MAX; }
   DEV void setup(int t0, int tid) {
-    const int lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-    for (int i = 0; i < NIW; i++) { kr[i] = G::krow(wave, i, lane); cl[i] = t0 + G::col(wave, i, lane); }
-  }
-  DEV void issue(int kt, char* tile) {
-    const int wave = threadIdx.x >> 6;
+    const int lane = tid & 63, wave = wave_id();
 #pragma unroll
     for (int i = 0; i < NIW; i++) {
-      int k = kt * BK + kr[i];
-      const void* src = (k < K && cl[i] < ncols) ? (const void*)(p + (long)k * ld + cl[i]) : zero_src();
-      glds16(src, tile + (wave * NIW + i) * 1024);
+      kr[i] = G::krow(wave, i, lane);
+      int cl = t0 + G::col(wave, i, lane);
+      cv[i] = cl < ncols;
+      vo[i] = (unsigned)(((long)kr[i] * ld + cl) * sizeof(T));
     }
   }
+  DEV void issue(int kt, char* tile) {
+    const int wave = wave_id();
+    const auto rs = make_rsrc(p, bytes());
+    const unsigned adv = (unsigned)((long)kt * BK * ld * sizeof(T));
+    if ((kt + 1) * BK > K) {          // K tail (uniform branch)
+#pragma unroll
+      for (int i = 0; i < NIW; i++) blds16(rs, cv[i] && kt * BK + kr[i] < K ? vo[i] + adv : BUF_OOB, tile + (wave * NIW + i) * 1024);
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < NIW; i++) blds16(rs, cv[i] ? vo[i] + adv : BUF_OOB, tile + (wave * NIW + i) * 1024);
+  }
+};
+
+// Incremental K-tile -> (tap, channel base) walker for gathers whose K is tap-major with
+// SC % BK == 0: a whole K tile then lies inside one tap, so tap/channel are wave-uniform.
+struct TapWalk {
+  int nk = -1, tap = 0, c0 = 0, th = 0, tw = 0;
+  // returns true when the tap changed (per-lane validity must be recomputed)
+  DEV bool step(int kt, int BK, int SC, int TW) {
+    if (kt != nk) {
+      int k = kt * BK; tap = k / SC; c0 = k - tap * SC; th = tap / TW; tw = tap - th * TW;
+      nk = kt + 1; return true;
+    }
+    nk = kt + 1;
+    c0 += BK;
+    if (c0 < SC) return false;
+    c0 = 0; tap++;
+    if (++tw == TW) { tw = 0; th++; }
+    return true;
+  }
+  // generic (SC % BK != 0, SC >= BK): advance by BK channels, a tile spans taps tap and tap+1
+  DEV void step_any(int kt, int BK, int SC, int TW) {
+    if (kt != nk) { int k = kt * BK; tap = k / SC; c0 = k - tap * SC; th = tap / TW; tw = tap - th * TW; }
+    else { c0 += BK; if (c0 >= SC) { c0 -= SC; tap++; if (++tw == TW) { tw = 0; th++; } } }
+    nk = kt + 1;
+  }
+  DEV void next_tap(int TW, int& th1, int& tw1) const { tw1 = tw + 1; th1 = th; if (tw1 == TW) { tw1 = 0; th1++; } }
 };
 
 // conv forward A operand: rows = output pixels (b,oy,ox) of RH x RW, k = tap*SC + c
@@ -178,31 +229,59 @@ template <typename T, int R, bool RELU_ = false> struct ConvFwdA {
   static constexpr bool KCL = true, RELU = RELU_;
   typedef KCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* x; ConvGeo g; int M; int relu;
-  int rb[NIW], ry[NIW], rx[NIW];
-  int tap[NIW], c[NIW];     // incremental k -> (tap, channel) per chunk
+  int iy0[NIW], ix0[NIW], pix0[NIW];      // top-left input pixel (may be outside) and its element offset + kel
+  int kl[NIW];
+  unsigned base[NIW];
+  TapWalk tw;
+  HD unsigned long bytes() const { return (unsigned long)g.B * g.SH * g.SW * g.SC * sizeof(T); }
+  HD bool buf_ok() const { return bytes() < BUF_MAX && g.SC >= BK; }
   DEV void setup(int t0, int tid) {
-    const int lane = tid & 63, wave = tid >> 6;
+    const int lane = tid & 63, wave = wave_id();
     int hw = g.RH * g.RW;
 #pragma unroll
     for (int i = 0; i < NIW; i++) {
       int m = t0 + G::row(wave, i, lane);
-      if (m < M) { int b = m / hw; int r = m - b * hw; int oy = r / g.RW; rb[i] = b; ry[i] = oy * g.s - g.p; rx[i] = (r - oy * g.RW) * g.s - g.p; }
-      else { rb[i] = -1; ry[i] = 0; rx[i] = 0; }
-      tap[i] = -1; c[i] = G::kel(wave, i, lane);
+      int kel = G::kel(wave, i, lane);
+      kl[i] = kel;
+      if (m < M) {
+        int b = m / hw; int r = m - b * hw; int oy = r / g.RW;
+        iy0[i] = oy * g.s - g.p; ix0[i] = (r - oy * g.RW) * g.s - g.p;
+        pix0[i] = ((b * g.SH + iy0[i]) * g.SW + ix0[i]) * g.SC + kel;
+      } else { iy0[i] = -0x4000000; ix0[i] = 0; pix0[i] = 0; }
     }
+    tw = TapWalk{};
   }
   DEV void issue(int kt, char* tile) {
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_id();
+    const auto rs = make_rsrc(x, bytes());
+    if (g.SC % BK) {                 // channels not a multiple of BK: per-lane tap (rare shapes)
+      tw.step_any(kt, BK, g.SC, g.KW);
+      int th1, tw1; tw.next_tap(g.KW, th1, tw1);
 #pragma unroll
-    for (int i = 0; i < NIW; i++) {
-      if (tap[i] < 0) { int k = kt * BK + c[i]; tap[i] = k / g.SC; c[i] = k - tap[i] * g.SC; }
-      int kh = tap[i] / g.KW, kw = tap[i] - kh * g.KW;
-      int iy = ry[i] + kh, ix = rx[i] + kw;
-      bool ok = tap[i] < g.KH * g.KW && rb[i] >= 0 && iy >= 0 && iy < g.SH && ix >= 0 && ix < g.SW;
-      const void* src = ok ? (const void*)(x + (((long)rb[i] * g.SH + iy) * g.SW + ix) * g.SC + c[i]) : zero_src();
-      glds16(src, tile + (wave * NIW + i) * 1024);
-      c[i] += BK; while (c[i] >= g.SC) { c[i] -= g.SC; tap[i]++; }
+      for (int i = 0; i < NIW; i++) {
+        int c = tw.c0 + kl[i];
+        bool wr = c >= g.SC;
+        int th = wr ? th1 : tw.th, tww = wr ? tw1 : tw.tw;
+        int iy = iy0[i] + th, ix = ix0[i] + tww;
+        bool ok = tw.tap + (int)wr < g.KH * g.KW && (unsigned)iy < (unsigned)g.SH && (unsigned)ix < (unsigned)g.SW;
+        int off = pix0[i] - kl[i] + (th * g.SW + tww) * g.SC + (wr ? c - g.SC : c);
+        blds16(rs, ok ? (unsigned)off * (unsigned)sizeof(T) : BUF_OOB, tile + (wave * NIW + i) * 1024);
+      }
+      return;
     }
+    if (tw.step(kt, BK, g.SC, g.KW)) {
+      const bool tv = tw.tap < g.KH * g.KW;
+      const int toff = (tw.th * g.SW + tw.tw) * g.SC;
+#pragma unroll
+      for (int i = 0; i < NIW; i++) {
+        int iy = iy0[i] + tw.th, ix = ix0[i] + tw.tw;
+        bool ok = tv && (unsigned)iy < (unsigned)g.SH && (unsigned)ix < (unsigned)g.SW;
+        base[i] = ok ? (unsigned)(pix0[i] + toff) * (unsigned)sizeof(T) : BUF_OOB;
+      }
+    }
+    const unsigned cb = (unsigned)(tw.c0 * sizeof(T));
+#pragma unroll
+    for (int i = 0; i < NIW; i++) blds16(rs, base[i] + cb, tile + (wave * NIW + i) * 1024);
   }
 };
 
@@ -212,31 +291,59 @@ template <typename T, int R> struct ConvDgradA {
   typedef KCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* dy; ConvGeo g; int M;
   int relu = 0;
-  int rb[NIW], ry[NIW], rx[NIW];
-  int tap[NIW], c[NIW];
+  int ry[NIW], rx[NIW], pix0[NIW], kl[NIW];
+  unsigned base[NIW];
+  TapWalk tw;
+  HD unsigned long bytes() const { return (unsigned long)g.B * g.SH * g.SW * g.SC * sizeof(T); }
+  HD bool buf_ok() const { return bytes() < BUF_MAX && g.SC >= BK; }
   DEV void setup(int t0, int tid) {
-    const int lane = tid & 63, wave = tid >> 6;
+    const int lane = tid & 63, wave = wave_id();
     int hw = g.RH * g.RW;
 #pragma unroll
     for (int i = 0; i < NIW; i++) {
       int m = t0 + G::row(wave, i, lane);
-      if (m < M) { int b = m / hw; int r = m - b * hw; int yy = r / g.RW; rb[i] = b; ry[i] = yy + g.qy0; rx[i] = (r - yy * g.RW) + g.qx0; }
-      else { rb[i] = -1; ry[i] = 0; rx[i] = 0; }
-      tap[i] = -1; c[i] = G::kel(wave, i, lane);
+      int kel = G::kel(wave, i, lane);
+      kl[i] = kel;
+      if (m < M) {
+        int b = m / hw; int r = m - b * hw; int yy = r / g.RW;
+        ry[i] = yy + g.qy0; rx[i] = (r - yy * g.RW) + g.qx0;
+        pix0[i] = ((b * g.SH + ry[i]) * g.SW + rx[i]) * g.SC + kel;
+      } else { ry[i] = -0x4000000; rx[i] = 0; pix0[i] = 0; }
     }
+    tw = TapWalk{};
   }
   DEV void issue(int kt, char* tile) {
-    const int wave = threadIdx.x >> 6;
+    const int wave = wave_id();
+    const auto rs = make_rsrc(dy, bytes());
+    const int TW = g.ntw > 0 ? g.ntw : 1;
+    if (g.SC % BK) {                 // channels not a multiple of BK: per-lane tap (rare shapes)
+      tw.step_any(kt, BK, g.SC, TW);
+      int th1, tw1; tw.next_tap(TW, th1, tw1);
 #pragma unroll
-    for (int i = 0; i < NIW; i++) {
-      if (tap[i] < 0) { int k = kt * BK + c[i]; tap[i] = k / g.SC; c[i] = k - tap[i] * g.SC; }
-      int jh = g.ntw ? tap[i] / g.ntw : 0, jw = tap[i] - jh * g.ntw;
-      int sy = ry[i] - jh, sx = rx[i] - jw;
-      bool ok = tap[i] < g.nth * g.ntw && rb[i] >= 0 && sy >= 0 && sy < g.SH && sx >= 0 && sx < g.SW;
-      const void* src = ok ? (const void*)(dy + (((long)rb[i] * g.SH + sy) * g.SW + sx) * g.SC + c[i]) : zero_src();
-      glds16(src, tile + (wave * NIW + i) * 1024);
-      c[i] += BK; while (c[i] >= g.SC) { c[i] -= g.SC; tap[i]++; }
+      for (int i = 0; i < NIW; i++) {
+        int c = tw.c0 + kl[i];
+        bool wr = c >= g.SC;
+        int th = wr ? th1 : tw.th, tww = wr ? tw1 : tw.tw;
+        int sy = ry[i] - th, sx = rx[i] - tww;
+        bool ok = tw.tap + (int)wr < g.nth * g.ntw && (unsigned)sy < (unsigned)g.SH && (unsigned)sx < (unsigned)g.SW;
+        int off = pix0[i] - kl[i] - (th * g.SW + tww) * g.SC + (wr ? c - g.SC : c);
+        blds16(rs, ok ? (unsigned)off * (unsigned)sizeof(T) : BUF_OOB, tile + (wave * NIW + i) * 1024);
+      }
+      return;
     }
+    if (tw.step(kt, BK, g.SC, TW)) {
+      const bool tv = tw.tap < g.nth * g.ntw;
+      const int toff = (tw.th * g.SW + tw.tw) * g.SC;
+#pragma unroll
+      for (int i = 0; i < NIW; i++) {
+        int sy = ry[i] - tw.th, sx = rx[i] - tw.tw;
+        bool ok = tv && (unsigned)sy < (unsigned)g.SH && (unsigned)sx < (unsigned)g.SW;
+        base[i] = ok ? (unsigned)(pix0[i] - toff) * (unsigned)sizeof(T) : BUF_OOB;
+      }
+    }
+    const unsigned cb = (unsigned)(tw.c0 * sizeof(T));
+#pragma unroll
+    for (int i = 0; i < NIW; i++) blds16(rs, base[i] + cb, tile + (wave * NIW + i) * 1024);
   }
 };
 
@@ -246,68 +353,117 @@ template <typename T, int R> struct ConvDgradB {
   typedef MCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* w; ConvGeo g; int NC;     // NC = output channels of the dgrad (= conv input channels)
   int relu = 0;
-  int kr[NIW], cl[NIW];
+  unsigned lo[NIW]; bool cv[NIW]; int kr[NIW];
+  TapWalk tw;
+  HD unsigned long bytes() const { return (unsigned long)g.SC * g.KH * g.KW * NC * sizeof(T); }
+  HD bool buf_ok() const { return bytes() < BUF_MAX && g.SC >= BK; }
   DEV void setup(int t0, int tid) {
-    const int lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-    for (int i = 0; i < NIW; i++) { kr[i] = G::krow(wave, i, lane); cl[i] = t0 + G::col(wave, i, lane); }
-  }
-  DEV void issue(int kt, char* tile) {
-    const int wave = threadIdx.x >> 6;
-    const int K = g.nth * g.ntw * g.SC;
+    const int lane = tid & 63, wave = wave_id();
 #pragma unroll
     for (int i = 0; i < NIW; i++) {
-      int k = kt * BK + kr[i];
-      const void* src = zero_src();
-      if (k < K && cl[i] < NC) {
-        int t = k / g.SC, cc = k - t * g.SC;
-        int jh = t / g.ntw, jw = t - jh * g.ntw;
-        int kh = g.kh0 + g.s * jh, kw = g.kw0 + g.s * jw;
-        src = (const void*)(w + (((long)cc * g.KH + kh) * g.KW + kw) * NC + cl[i]);
-      }
-      glds16(src, tile + (wave * NIW + i) * 1024);
+      kr[i] = G::krow(wave, i, lane); int cl = t0 + G::col(wave, i, lane);
+      cv[i] = cl < NC;
+      lo[i] = (unsigned)(((long)kr[i] * g.KH * g.KW * NC + cl) * sizeof(T));
     }
+    tw = TapWalk{};
+  }
+  DEV void issue(int kt, char* tile) {
+    const int wave = wave_id();
+    const auto rs = make_rsrc(w, bytes());
+    const int TW = g.ntw > 0 ? g.ntw : 1;
+    if (g.SC % BK) {                 // a tile spans taps tap / tap+1 (rows c0+kr >= SC wrap)
+      tw.step_any(kt, BK, g.SC, TW);
+      int th1, tw1; tw.next_tap(TW, th1, tw1);
+      const int kh = g.kh0 + g.s * tw.th, kw = g.kw0 + g.s * tw.tw;
+      const int kh1 = g.kh0 + g.s * th1, kw1 = g.kw0 + g.s * tw1;
+      const bool tv0 = tw.tap < g.nth * g.ntw, tv1 = tw.tap + 1 < g.nth * g.ntw;
+      const unsigned u0 = (unsigned)((((long)tw.c0 * g.KH + kh) * g.KW + kw) * NC * sizeof(T));
+      const unsigned u1 = (unsigned)((((long)(tw.c0 - g.SC) * g.KH + kh1) * g.KW + kw1) * NC * sizeof(T));
+#pragma unroll
+      for (int i = 0; i < NIW; i++) {
+        bool wr = tw.c0 + kr[i] >= g.SC;
+        bool ok = cv[i] && (wr ? tv1 : tv0);
+        blds16(rs, ok ? lo[i] + (wr ? u1 : u0) : BUF_OOB, tile + (wave * NIW + i) * 1024);
+      }
+      return;
+    }
+    tw.step(kt, BK, g.SC, TW);
+    const bool tv = tw.tap < g.nth * g.ntw;
+    const int kh = g.kh0 + g.s * tw.th, kw = g.kw0 + g.s * tw.tw;
+    const unsigned uo = (unsigned)((((long)tw.c0 * g.KH + kh) * g.KW + kw) * NC * sizeof(T));
+#pragma unroll
+    for (int i = 0; i < NIW; i++) blds16(rs, (tv && cv[i]) ? lo[i] + uo : BUF_OOB, tile + (wave * NIW + i) * 1024);
   }
 };
 
 // wgrad B operand (MC gather): B[k=pix of the conv output grid RH x RW][n=(tap, cin)] = X[src][cin]
+// Fast path (RW % BK == 0): the 64 pixels of a K tile share one output row, so (b, oy, ox0) are
+// wave-uniform and interior tiles need no per-lane bounds test.
 template <typename T, int R, bool RELU_ = false> struct WgradB {
   static constexpr bool KCL = false, RELU = RELU_;
   typedef MCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* x; ConvGeo g; int NPIX; int relu;   // g.SC = Cin of X, g.SH/SW = X dims, RH/RW = output grid
-  int kh[NIW], kw[NIW], cin[NIW], kr[NIW]; bool cval[NIW];
-  int pb[NIW], py[NIW], pxx[NIW]; int started;
+  int kh[NIW], kw[NIW], kr[NIW], cin[NIW]; unsigned lo[NIW]; bool cval[NIW];
+  int nk, pb, poy, pox;                         // uniform walker (fast path)
+  int qb[NIW], qy[NIW], qx[NIW];                // per-lane walker (generic path)
+  HD unsigned long bytes() const { return (unsigned long)g.B * g.SH * g.SW * g.SC * sizeof(T); }
+  HD bool buf_ok() const { return bytes() < BUF_MAX; }
   DEV void setup(int t0, int tid) {
-    const int lane = tid & 63, wave = tid >> 6;
+    const int lane = tid & 63, wave = wave_id();
 #pragma unroll
     for (int i = 0; i < NIW; i++) {
       int col = t0 + G::col(wave, i, lane);
       kr[i] = G::krow(wave, i, lane);
       int tp = col / g.SC; cin[i] = col - tp * g.SC; kh[i] = tp / g.KW; kw[i] = tp - kh[i] * g.KW;
       cval[i] = tp < g.KH * g.KW;
+      // lane part of the source offset for an interior tile: (kh*SW + kw + kr*s)*SC + cin
+      lo[i] = (unsigned)(((long)(kh[i] * g.SW + kw[i] + kr[i] * g.s) * g.SC + cin[i]) * sizeof(T));
     }
-    started = 0;
+    nk = -1;
   }
   DEV void issue(int kt, char* tile) {
-    const int wave = threadIdx.x >> 6;
-    if (!started) {
-      started = 1;
+    const int wave = wave_id();
+    const auto rs = make_rsrc(x, bytes());
+    if (g.RW % BK == 0) {
+      if (kt != nk) { int k = kt * BK; int hw = g.RH * g.RW; pb = k / hw; int r = k - pb * hw; poy = r / g.RW; pox = r - poy * g.RW; }
+      else { pox += BK; if (pox >= g.RW) { pox = 0; if (++poy >= g.RH) { poy = 0; pb++; } } }
+      nk = kt + 1;
+      const int iy0 = poy * g.s - g.p, ix0 = pox * g.s - g.p;
+      const bool live = pb < g.B;
+      const unsigned uo = (unsigned)((((long)pb * g.SH + iy0) * g.SW + ix0) * g.SC * (long)sizeof(T));
+      const bool interior = iy0 >= 0 && iy0 + g.KH <= g.SH && ix0 >= 0 && ix0 + (BK - 1) * g.s + g.KW <= g.SW;
+      if (live && interior) {
+#pragma unroll
+        for (int i = 0; i < NIW; i++) blds16(rs, cval[i] ? lo[i] + uo : BUF_OOB, tile + (wave * NIW + i) * 1024);
+      } else {
+#pragma unroll
+        for (int i = 0; i < NIW; i++) {
+          int iy = iy0 + kh[i], ix = ix0 + kr[i] * g.s + kw[i];
+          bool ok = live && cval[i] && (unsigned)iy < (unsigned)g.SH && (unsigned)ix < (unsigned)g.SW;
+          blds16(rs, ok ? lo[i] + uo : BUF_OOB, tile + (wave * NIW + i) * 1024);
+        }
+      }
+      return;
+    }
+    // generic: per-lane pixel walker
+    if (kt != nk) {
       const int hw = g.RH * g.RW;
 #pragma unroll
       for (int i = 0; i < NIW; i++) {
         int k = kt * BK + kr[i];
         int b = k / hw; int r = k - b * hw; int oy = r / g.RW;
-        pb[i] = b; py[i] = oy; pxx[i] = r - oy * g.RW;
+        qb[i] = b; qy[i] = oy; qx[i] = r - oy * g.RW;
       }
     }
+    nk = kt + 1;
 #pragma unroll
     for (int i = 0; i < NIW; i++) {
-      int iy = py[i] * g.s - g.p + kh[i], ix = pxx[i] * g.s - g.p + kw[i];
-      bool ok = cval[i] && pb[i] < g.B && iy >= 0 && iy < g.SH && ix >= 0 && ix < g.SW;
-      const void* src = ok ? (const void*)(x + (((long)pb[i] * g.SH + iy) * g.SW + ix) * g.SC + cin[i]) : zero_src();
-      glds16(src, tile + (wave * NIW + i) * 1024);
-      pxx[i] += BK;
-      while (pxx[i] >= g.RW) { pxx[i] -= g.RW; if (++py[i] >= g.RH) { py[i] = 0; pb[i]++; } }
+      int iy = qy[i] * g.s - g.p + kh[i], ix = qx[i] * g.s - g.p + kw[i];
+      bool ok = cval[i] && qb[i] < g.B && (unsigned)iy < (unsigned)g.SH && (unsigned)ix < (unsigned)g.SW;
+      unsigned v = (unsigned)(((((long)qb[i] * g.SH + iy) * g.SW + ix) * g.SC + cin[i]) * (long)sizeof(T));
+      blds16(rs, ok ? v : BUF_OOB, tile + (wave * NIW + i) * 1024);
+      qx[i] += BK;
+      while (qx[i] >= g.RW) { qx[i] -= g.RW; if (++qy[i] >= g.RH) { qy[i] = 0; qb[i]++; } }
     }
     (void)NPIX;
   }
@@ -409,7 +565,7 @@ template <typename T, int BM, int BN, int NST, class LA, class LB, class EPI>
 __global__ void __launch_bounds__(GEMM_THREADS) igemm_kernel(LA la, LB lb, EPI epi, int KTILES, int split) {
   typedef GemmShape<T, BM, BN, NST> S;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int wm = wave / S::WN, wn = wave % S::WN;
   constexpr int MI = S::MI, NI = S::NI, KS = Mma<T>::KSTEPS;
   constexpr int NL = LA::NIW + LB::NIW;       // LDS-DMA instructions per thread per K tile
@@ -605,6 +761,10 @@ struct EpiWgrad {
 template <typename T, int BM, int BN, class LA, class LB, class EPI, int NST = 3>
 static int launch_igemm(LA la, LB lb, EPI epi, int M, int N, int KTILES, int split, int zdim_extra, hipStream_t st) {
   typedef GemmShape<T, BM, BN, NST> S;
+  if (!la.buf_ok() || !lb.buf_ok()) {
+    s3od_set_error("igemm: operand too large for a buffer descriptor or gather channels < %d", KT<T>::BK);
+    return 22;
+  }
   auto kfn = igemm_kernel<T, BM, BN, NST, LA, LB, EPI>;
   static bool attr = false;
   if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS); attr = true; }
