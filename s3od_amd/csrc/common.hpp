@@ -81,4 +81,17 @@ DEV float gelu_erf_grad(float x) {
   return cdf + x * pdf;
 }
 
+// integer dev knob read once from the environment (micro-benchmark sweeps only; default otherwise)
+#include <stdlib.h>
+static inline int dev_knob(const char* name, int def) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : def;
+}
+
+// Column reductions over many workgroups add into S3OD_NREP replicas of the accumulator
+// (workgroup b -> replica b % S3OD_NREP) and a second pass folds the replicas: fp32/fp64 atomics
+// from ~1000 workgroups onto the same few KB serialise at the memory side (measured 2-3x slower
+// end to end for the BN backward / q,v-bias reductions).
+constexpr int S3OD_NREP = 32;
+
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

@@ -3,6 +3,7 @@
 // IoU-score MLP head fwd/bwd, mask-head backward prologue, ReLU masks.
 // Reference: src/s3od/model.py:109-467.
 #include "common.hpp"
+#include <type_traits>
 
 #define DISPATCH_T(dtype, ...)                                                  \
   do {                                                                          \
@@ -75,65 +76,151 @@ __global__ void affine_act_kernel(const T* __restrict__ x, const float* __restri
   store8<T>(y + i, v);
 }
 
-// BN backward, pass 1: per channel sums of dy' and dy'*xhat where dy' = dy (or dy*(y>0) if relu_y)
-// xhat = (z - mean)*rstd.  Output double [2][C].
-template <typename T>
-__global__ void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ z, const T* __restrict__ y_relu,
+// Row-blocked NHWC reductions: a 256-thread block = CG = C/8 column groups x (256/CG) row phases,
+// each thread owning 8 channels; per-thread partials are reduced over the row phases in LDS so a
+// block issues one atomic per channel (not one per thread).
+template <int NV> DEV void rowphase_reduce(float (&v)[NV][8], float* red, int t, int CG) {
+  const int nph = 256 / CG;
+#pragma unroll
+  for (int j = 0; j < NV; j++) {
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; e++) red[t * 8 + e] = v[j][e];
+    __syncthreads();
+    if (t < CG)
+      for (int q = 1; q < nph; q++)
+#pragma unroll
+        for (int e = 0; e < 8; e++) v[j][e] += red[(q * CG + t) * 8 + e];
+  }
+}
+
+// BN backward, pass 1: per channel sums of dy' and dy'*xhat where dy' = dy (or dy*(y>0) if RELU)
+// xhat = (z - mean)*rstd.  Output double [2][C].  Main loop keeps 4 pixel rows of loads in flight.
+template <typename T, bool RELU>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ z, const T* __restrict__ y_relu,
                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                      double* __restrict__ sums, long npix, int C, int pix_per_block) {
-  // block: 256 threads = (C/8) column groups x rows
+  __shared__ float red[256 * 8];
   const int cg = C / 8, rows = 256 / cg;
   const int t = threadIdx.x, cgi = t % cg, ri = t / cg;
-  if (ri >= rows) return;
   const int c = cgi * 8;
   float mu[8], rs[8];
   load8<float>(mean + c, mu); load8<float>(rstd + c, rs);
-  float s1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, s2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  long p0 = (long)blockIdx.x * pix_per_block, p1 = min(npix, p0 + pix_per_block);
-#pragma unroll 4
-  for (long p = p0 + ri; p < p1; p += rows) {
-    float d[8], zz[8];
-    load8<T>(dy + p * C + c, d); load8<T>(z + p * C + c, zz);
-    if (y_relu) { float yy[8]; load8<T>(y_relu + p * C + c, yy);
+  float acc[2][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0}};
+  const long p0 = (long)blockIdx.x * pix_per_block, p1 = min(npix, p0 + pix_per_block);
+  auto body = [&](const float* d0, const float* zz, const float* yy) {
 #pragma unroll
-      for (int e = 0; e < 8; e++) if (!(yy[e] > 0.f)) d[e] = 0.f; }
+    for (int e = 0; e < 8; e++) {
+      float d = (RELU && !(yy[e] > 0.f)) ? 0.f : d0[e];
+      float xh = (zz[e] - mu[e]) * rs[e];
+      acc[0][e] += d; acc[1][e] += d * xh;
+    }
+  };
+  long p = p0 + ri;
+  for (; p + 3 * rows < p1; p += 4 * rows) {
+    float d[4][8], zz[4][8], yy[4][8];
 #pragma unroll
-    for (int e = 0; e < 8; e++) { float xh = (zz[e] - mu[e]) * rs[e]; s1[e] += d[e]; s2[e] += d[e] * xh; }
+    for (int j = 0; j < 4; j++) {
+      const long o = (p + j * rows) * C + c;
+      load8<T>(dy + o, d[j]); load8<T>(z + o, zz[j]);
+      if (RELU) load8<T>(y_relu + o, yy[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) body(d[j], zz[j], yy[j]);
   }
+  for (; p < p1; p += rows) {
+    float d[8], zz[8], yy[8];
+    const long o = p * C + c;
+    load8<T>(dy + o, d); load8<T>(z + o, zz);
+    if (RELU) load8<T>(y_relu + o, yy);
+    body(d, zz, yy);
+  }
+  rowphase_reduce<2>(acc, red, t, cg);
+  if (t < cg) {
+    double* rep = sums + (long)(blockIdx.x % S3OD_NREP) * 3 * C;
 #pragma unroll
-  for (int e = 0; e < 8; e++) { atomicAdd(sums + c + e, (double)s1[e]); atomicAdd(sums + C + c + e, (double)s2[e]); }
+    for (int e = 0; e < 8; e++) { atomicAdd(rep + c + e, (double)acc[0][e]); atomicAdd(rep + C + c + e, (double)acc[1][e]); }
+  }
 }
 
-// BN backward, pass 2: dz = w*rstd*(dy' - s1/n - xhat*s2/n); also dw = s2, db = s1 (finalize)
-template <typename T>
-__global__ void bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ z, const T* __restrict__ y_relu,
+// fold the replicas of [s1 | s2] into replica 0
+__global__ void bn_fold_replicas_kernel(double* sums, int C) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * C) return;
+  double s = sums[i];
+  for (int r = 1; r < S3OD_NREP; r++) s += sums[(long)r * 3 * C + i];
+  sums[i] = s;
+}
+
+// BN backward, pass 2: dz = w*rstd*(dy' - s1/n - xhat*s2/n); optional dcb[c] += sum_p dz (the
+// bias gradient of the conv that produced z).
+template <typename T, bool RELU>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ z, const T* __restrict__ y_relu,
                                     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ w,
-                                    const double* __restrict__ sums, T* __restrict__ dz, long total, int C, long npix) {
-  long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  if (i >= total) return;
-  int c = i % C;
-  float d[8], zz[8];
-  load8<T>(dy + i, d); load8<T>(z + i, zz);
-  if (y_relu) { float yy[8]; load8<T>(y_relu + i, yy);
-#pragma unroll
-    for (int e = 0; e < 8; e++) if (!(yy[e] > 0.f)) d[e] = 0.f; }
-  float o[8];
+                                    double* __restrict__ sums, T* __restrict__ dz, float* __restrict__ dcb,
+                                    long npix, int C, int pix_per_block) {
+  __shared__ float red[256 * 8];
+  const int cg = C / 8, rows = 256 / cg;
+  const int t = threadIdx.x, cgi = t % cg, ri = t / cg;
+  const int c = cgi * 8;
+  float mu[8], rs[8], k1[8], m1[8], m2[8];
 #pragma unroll
   for (int e = 0; e < 8; e++) {
-    int cc = c + e;
-    float mu = mean[cc], rs = rstd[cc];
-    float m1 = (float)(sums[cc] / (double)npix), m2 = (float)(sums[C + cc] / (double)npix);
-    float xh = (zz[e] - mu) * rs;
-    o[e] = w[cc] * rs * (d[e] - m1 - xh * m2);
+    mu[e] = mean[c + e]; rs[e] = rstd[c + e]; k1[e] = w[c + e] * rs[e];
+    m1[e] = (float)(sums[c + e] / (double)npix); m2[e] = (float)(sums[C + c + e] / (double)npix);
   }
-  store8<T>(dz + i, o);
+  float acc[1][8] = {{0, 0, 0, 0, 0, 0, 0, 0}};
+  const long p0 = (long)blockIdx.x * pix_per_block, p1 = min(npix, p0 + pix_per_block);
+  auto body = [&](long o, const float* d0, const float* zz, const float* yy) {
+    float out[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      float d = (RELU && !(yy[e] > 0.f)) ? 0.f : d0[e];
+      float xh = (zz[e] - mu[e]) * rs[e];
+      out[e] = k1[e] * (d - m1[e] - xh * m2[e]);
+      acc[0][e] += out[e];
+    }
+    store8<T>(dz + o, out);
+  };
+  long p = p0 + ri;
+  for (; p + 3 * rows < p1; p += 4 * rows) {
+    float d[4][8], zz[4][8], yy[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const long o = (p + j * rows) * C + c;
+      load8<T>(dy + o, d[j]); load8<T>(z + o, zz[j]);
+      if (RELU) load8<T>(y_relu + o, yy[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) body((p + j * rows) * C + c, d[j], zz[j], yy[j]);
+  }
+  for (; p < p1; p += rows) {
+    float d[8], zz[8], yy[8];
+    const long o = p * C + c;
+    load8<T>(dy + o, d); load8<T>(z + o, zz);
+    if (RELU) load8<T>(y_relu + o, yy);
+    body(o, d, zz, yy);
+  }
+  if (dcb) {
+    rowphase_reduce<1>(acc, red, t, cg);
+    if (t < cg) {
+      double* rep = sums + (long)(blockIdx.x % S3OD_NREP) * 3 * C + 2 * C;
+#pragma unroll
+      for (int e = 0; e < 8; e++) atomicAdd(rep + c + e, (double)acc[0][e]);
+    }
+  }
 }
 
-__global__ void bn_param_grads_kernel(const double* sums, float* dw, float* db, int C) {
+__global__ void bn_param_grads_kernel(const double* sums, float* dw, float* db, float* dcb, int C) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   db[c] += (float)sums[c];
   dw[c] += (float)sums[C + c];
+  if (dcb) {
+    double s = 0.0;
+    for (int r = 0; r < S3OD_NREP; r++) s += sums[(long)r * 3 * C + 2 * C + c];
+    dcb[c] += (float)s;
+  }
 }
 
 // ---------------------------------------------------------------- bilinear (align_corners=False)
@@ -202,22 +289,25 @@ __global__ void bilinear_bwd_kernel(const T* __restrict__ dy, const float* __res
 // ---------------------------------------------------------------- pooled IoU head
 // mean over pixels: x [B, HW, C] -> out [B, C] f32 (atomics; out must be zeroed)
 template <typename T>
-__global__ void avgpool_kernel(const T* __restrict__ x, float* __restrict__ out, int HW, int C, int pix_per_block) {
+__global__ void __launch_bounds__(256) avgpool_kernel(const T* __restrict__ x, float* __restrict__ out, int HW, int C, int pix_per_block) {
+  __shared__ float red[256 * 8];
   const int cg = C / 8, rows = 256 / cg;
   const int t = threadIdx.x, cgi = t % cg, ri = t / cg;
-  if (ri >= rows) return;
   const int b = blockIdx.y, c = cgi * 8;
-  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float s[1][8] = {{0, 0, 0, 0, 0, 0, 0, 0}};
   long p0 = (long)blockIdx.x * pix_per_block, p1 = min((long)HW, p0 + pix_per_block);
 #pragma unroll 4
   for (long p = p0 + ri; p < p1; p += rows) {
     float v[8]; load8<T>(x + ((long)b * HW + p) * C + c, v);
 #pragma unroll
-    for (int e = 0; e < 8; e++) s[e] += v[e];
+    for (int e = 0; e < 8; e++) s[0][e] += v[e];
   }
-  float inv = 1.0f / (float)HW;
+  rowphase_reduce<1>(s, red, t, cg);
+  if (t < cg) {
+    float inv = 1.0f / (float)HW;
 #pragma unroll
-  for (int e = 0; e < 8; e++) atomicAdd(out + (long)b * C + c + e, s[e] * inv);
+    for (int e = 0; e < 8; e++) atomicAdd(out + (long)b * C + c + e, s[0][e] * inv);
+  }
 }
 
 // classifier_head (src/s3od/model.py:185-191): Linear(256,64) -> ReLU -> Linear(64,3); one block per image
@@ -264,30 +354,57 @@ __global__ void iou_head_bwd_kernel(const float* pooled, const float* hid, const
 }
 
 // ---------------------------------------------------------------- mask-head backward prologue
-// dlogits [B,3,HW] f32, h [M,96] T (post-ReLU) -> dh [M,96] T, dw2 [3][32], db2 [3] (accumulate)
+// dlogits [B,3,HW] f32, h [M,96] T (post-ReLU) -> dh [M,96] T = relu'(h) * dlogit_k * w2[k];
+// accumulates dw2 [3][32], db2 [3] and db1 [96] (= column sums of dh, the 3x3 convs' bias gradient).
+// block = 384 threads = 32 pixel rows x 12 chunks of 8 channels (chunk j belongs to head j/4).
 template <typename T>
-__global__ void mask_heads_bwd_kernel(const float* __restrict__ dlog, const T* __restrict__ hs, const float* __restrict__ w2,
-                                      T* __restrict__ dh, float* __restrict__ dw2, float* __restrict__ db2, long M, int HW, int pix_per_block) {
-  __shared__ float sw[96], sb[3];
-  const int t = threadIdx.x;   // 96 threads: column j
-  if (t < 96) sw[t] = 0.f;
-  if (t < 3) sb[t] = 0.f;
-  __syncthreads();
-  const int k = t / 32;
-  const float wk = w2[t];
-  float accw = 0.f, accb = 0.f;
-  long p0 = (long)blockIdx.x * pix_per_block, p1 = min(M, p0 + pix_per_block);
-#pragma unroll 4
-  for (long m = p0; m < p1; m++) {
+__global__ void __launch_bounds__(384) mask_heads_bwd_kernel(const float* __restrict__ dlog, const T* __restrict__ hs,
+                                                             const float* __restrict__ w2, T* __restrict__ dh,
+                                                             float* __restrict__ dw2, float* __restrict__ db2, float* __restrict__ db1,
+                                                             long M, int HW) {
+  __shared__ float red[384 * 8];
+  const int t = threadIdx.x, j = t % 12, pr = t / 12;
+  const int k = j >> 2, c0 = j * 8;
+  float wk[8];
+  load8<float>(w2 + c0, wk);
+  float aw[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ab[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float adb = 0.f;
+  for (long m = (long)blockIdx.x * 32 + pr; m < M; m += (long)gridDim.x * 32) {
     int b = m / HW; long pix = m - (long)b * HW;
     float dl = dlog[((long)b * 3 + k) * HW + pix];
-    float hv = to_f<T>(hs[m * 96 + t]);
-    dh[m * 96 + t] = from_f<T>(hv > 0.f ? dl * wk : 0.f);
-    accw += dl * hv;
-    if ((t & 31) == 0) accb += dl;
+    float hv[8], o[8];
+    load8<T>(hs + m * 96 + c0, hv);
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      o[e] = hv[e] > 0.f ? dl * wk[e] : 0.f;
+      aw[e] += dl * hv[e];
+    }
+    store8<T>(dh + m * 96 + c0, o);
+#pragma unroll
+    for (int e = 0; e < 8; e++) ab[e] += o[e];
+    adb += dl;
   }
-  atomicAdd(dw2 + t, accw);
-  if ((t & 31) == 0) atomicAdd(db2 + k, accb);
+  // reduce over the 32 pixel rows: aw -> dw2, ab -> db1, adb (chunks 0,4,8) -> db2
+  float* r = red;
+  for (int pass = 0; pass < 3; pass++) {
+    __syncthreads();
+    if (pass == 0) { for (int e = 0; e < 8; e++) r[t * 8 + e] = aw[e]; }
+    else if (pass == 1) { for (int e = 0; e < 8; e++) r[t * 8 + e] = ab[e]; }
+    else r[t * 8] = adb;
+    __syncthreads();
+    if (t < 96) {
+      const int jj = t >> 3, e = t & 7;
+      if (pass < 2) {
+        float s = 0.f;
+        for (int q = 0; q < 32; q++) s += r[((q * 12) + jj) * 8 + e];
+        atomicAdd((pass == 0 ? dw2 : db1) + t, s);
+      } else if (t < 3) {
+        float s = 0.f;
+        for (int q = 0; q < 32; q++) s += r[((q * 12) + 4 * t) * 8];
+        atomicAdd(db2 + t, s);
+      }
+    }
+  }
 }
 
 extern "C" {
@@ -323,19 +440,29 @@ int s3od_affine_act(int dtype, const void* x, const float* scale, const float* s
   return s3od_check_launch("affine_act");
 }
 
+// sums: workspace of S3OD_NREP * 3 * C doubles (replicated [s1 | s2 | conv-bias] accumulators)
 int s3od_bn_bwd(int dtype, const void* dy, const void* z, const void* y_relu, const float* mean, const float* rstd,
-                const float* w, double* sums, void* dz, float* dw, float* db, long npix, int C, void* stream) {
+                const float* w, double* sums, void* dz, float* dw, float* db, float* dcb, long npix, int C, void* stream) {
   S3OD_REQUIRE(C % 8 == 0 && 256 % (C / 8) == 0, "bn_bwd: C");
   hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(sums, 0, sizeof(double) * 2 * C, st);
-  const int ppb = 4096;
+  (void)hipMemsetAsync(sums, 0, sizeof(double) * S3OD_NREP * 3 * C, st);
+  // ~512 blocks for large maps (measured optimum: fewer starve HBM, more pay atomics), >= 64 pixels per block
+  const int rows = 256 / (C / 8);
+  long ppb = max(64L, npix / dev_knob("S3OD_BN_BLOCKS", 512));
+  ppb = (ppb + rows - 1) / rows * rows;
+  const int nb = cdiv(npix, ppb);
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(cdiv(npix, ppb)), dim3(256), 0, st, (const T*)dy, (const T*)z, (const T*)y_relu,
-                       mean, rstd, sums, npix, C, ppb);
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(cdiv(npix * C / 8, 256)), dim3(256), 0, st, (const T*)dy, (const T*)z,
-                       (const T*)y_relu, mean, rstd, w, sums, (T*)dz, npix * C, C, npix);
+    auto go = [&](auto relu) {
+      constexpr bool R = decltype(relu)::value;
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, R>), dim3(nb), dim3(256), 0, st, (const T*)dy, (const T*)z, (const T*)y_relu,
+                         mean, rstd, sums, npix, C, (int)ppb);
+      hipLaunchKernelGGL(bn_fold_replicas_kernel, dim3(cdiv(2 * C, 256)), dim3(256), 0, st, sums, C);
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, R>), dim3(nb), dim3(256), 0, st, (const T*)dy, (const T*)z,
+                         (const T*)y_relu, mean, rstd, w, sums, (T*)dz, dcb, npix, C, (int)ppb);
+    };
+    if (y_relu) go(std::true_type{}); else go(std::false_type{});
   });
-  hipLaunchKernelGGL(bn_param_grads_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, dw, db, C);
+  hipLaunchKernelGGL(bn_param_grads_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, dw, db, dcb, C);
   return s3od_check_launch("bn_bwd");
 }
 
@@ -383,12 +510,12 @@ int s3od_iou_head_bwd(const float* pooled, const float* hid, const float* w1, co
 }
 
 int s3od_mask_heads_bwd(int dtype, const float* dlogits, const void* hsave, const float* w2, void* dh, float* dw2, float* db2,
-                        int B, int HW, void* stream) {
+                        float* db1, int B, int HW, void* stream) {
   long M = (long)B * HW;
-  const int ppb = 128;
+  const int nb = (int)min(1024L, (M + 31) / 32);
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(mask_heads_bwd_kernel<T>, dim3(cdiv(M, ppb)), dim3(96), 0, (hipStream_t)stream, dlogits, (const T*)hsave, w2,
-                       (T*)dh, dw2, db2, M, HW, ppb);
+    hipLaunchKernelGGL(mask_heads_bwd_kernel<T>, dim3(nb), dim3(384), 0, (hipStream_t)stream, dlogits, (const T*)hsave, w2,
+                       (T*)dh, dw2, db2, db1, M, HW);
   });
   return s3od_check_launch("mask_heads_bwd");
 }

@@ -696,8 +696,12 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
   double* stats;                        // optional: [2][N] (sum, sumsq) of pre (BN batch statistics)
   int act, M, N;
   RowMap rm;
+  float* csum = nullptr;                // optional: out[n] column sums (bias gradient), fp32 atomics
   DEV void prepare(int) {}
   DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN) const {
+    // a thread always sees the same 8-column group (GEMM_THREADS % (BN/8) == 0), so its column
+    // partial sums live in registers until the block reduction below
+    float cs8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for_segments(ct, LDT, BM, BN, m0, n0, M, N, tid, [&](int m, int n, const float* a, int, int) {
       float pv[8], v[8], o[8];
       long orow = rm.map(m);
@@ -719,6 +723,10 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
 #pragma unroll
         for (int e = 0; e < 8; e++) o[e] += r[e]; }
       store8<TO>(out + orow * ldo + coff + n, o);
+      if (csum) {
+#pragma unroll
+        for (int e = 0; e < 8; e++) cs8[e] += o[e];
+      }
     });
     if (stats) {
       // column statistics of pre over this tile's valid rows: 256 threads -> (col, row-phase)
@@ -735,6 +743,21 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
         }
         atomicAdd(stats + n, (double)s);
         atomicAdd(stats + N + n, (double)q);
+      }
+    }
+    if (csum) {
+      // reduce the per-thread 8-column partials over the row phases through the (consumed) C tile
+      __syncthreads();
+      float* red = (float*)ct;
+#pragma unroll
+      for (int e = 0; e < 8; e++) red[tid * 8 + e] = cs8[e];
+      __syncthreads();
+      const int spr = BN / 8, nph = GEMM_THREADS / spr;
+      if (tid < BN && n0 + tid < N) {
+        const int g = tid >> 3, e = tid & 7;
+        float s = 0.f;
+        for (int ph = 0; ph < nph; ph++) s += red[(ph * spr + g) * 8 + e];
+        atomicAdd(csum + n0 + tid, s);
       }
     }
   }

@@ -105,6 +105,15 @@ template <typename T> struct EpiHeads {
 
 template <int BM, int BN> struct Tile {};
 
+// dw[(co*Cin + ci)*taps + tap] += ws[(co*taps + tap)*Cin + ci]   (one thread per dw element)
+__global__ void wgrad_permute_add_kernel(const float* __restrict__ ws, float* __restrict__ dw, int Cout, int Cin, int taps) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)Cout * Cin * taps) return;
+  int tap = i % taps; long r = i / taps;
+  int ci = r % Cin; int co = r / Cin;
+  dw[i] += ws[((long)co * taps + tap) * Cin + ci];
+}
+
 extern "C" {
 
 // ---------------------------------------------------------------------------------- linear
@@ -144,7 +153,7 @@ int s3od_linear_fwd(int dtype, int M, int N, int K, const void* x, long ldx, con
 // gelu'(aux); with act=ACT_NONE a non-null aux is ADDED (aux may alias dx: in-place accumulate).
 int s3od_linear_dgrad(int dtype, int M, int N, int K, const void* dy, long lddy, const void* w,
                       int act, const void* aux, long ldaux, void* dx, long lddx, int out_f32,
-                      int row_mode, int P, int prefix, void* stream) {
+                      int row_mode, int P, int prefix, float* colsum, void* stream) {
   S3OD_REQUIRE(K % 8 == 0 && N % 8 == 0, "linear_dgrad: K,N %% 8");
   RowMap rm = dense_rm(); rm.mode = row_mode; rm.P = P; rm.prefix = prefix;
   hipStream_t st = (hipStream_t)stream;
@@ -156,10 +165,10 @@ int s3od_linear_dgrad(int dtype, int M, int N, int K, const void* dy, long lddy,
       DenseMC<T, BN> lb{(const T*)w, (long)N, K, N};
       if (out_f32) {
         // f32 output: aux is an f32 tensor to add (e.g. the residual-stream gradient, in place)
-        EpiStd<float, float> e{(float*)dx, lddx, 0, nullptr, nullptr, nullptr, (const float*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, rm};
+        EpiStd<float, float> e{(float*)dx, lddx, 0, nullptr, nullptr, nullptr, (const float*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, rm, colsum};
         return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, KTILES, 1, 1, st);
       }
-      EpiStd<T, T> e{(T*)dx, lddx, 0, nullptr, nullptr, nullptr, (const T*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, rm};
+      EpiStd<T, T> e{(T*)dx, lddx, 0, nullptr, nullptr, nullptr, (const T*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, rm, colsum};
       return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, KTILES, 1, 1, st);
     });
   });
@@ -210,7 +219,7 @@ int s3od_qkv_rope_fwd(int dtype, int B, int Ntok, int P, const void* x, const vo
 int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW,
                   int stride, int pad, const void* x, int relu_in, const void* wp,
                   const float* bias, const float* scale, const float* shift, int act, const void* res1, const void* res2,
-                  void* out, void* pre, double* stats, void* stream) {
+                  void* out, void* pre, double* stats, float* colsum, void* stream) {
   S3OD_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "conv_fwd: channels %% 8 (Cin=%d Cout=%d)", Cin, Cout);
   ConvGeo g{}; g.B = B; g.SH = H; g.SW = W; g.SC = Cin; g.RH = OH; g.RW = OW; g.KH = KH; g.KW = KW; g.s = stride; g.p = pad;
   const int M = B * OH * OW, N = Cout, K = KH * KW * Cin;
@@ -224,7 +233,7 @@ int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int C
         ConvFwdA<T, BM, decltype(rl)::value> la{}; la.x = (const T*)x; la.g = g; la.M = M; la.relu = relu_in;
         DenseKC<T, BN> lb{(const T*)wp, (long)K, N, K, 0};
         EpiStd<T, T> e{(T*)out, (long)Cout, 0, bias, scale, shift, (const T*)res1, (long)Cout, (const T*)res2, (long)Cout,
-                       (T*)pre, (long)Cout, stats, act, M, N, dense_rm()};
+                       (T*)pre, (long)Cout, stats, act, M, N, dense_rm(), colsum};
         return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, KTILES, 1, 1, st);
       });
     };
@@ -243,7 +252,7 @@ int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int C
 int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW,
                     int stride, int pad, const void* dy, const void* wp,
                     const float* bias, const float* scale, const float* shift, int act, const void* res1,
-                    const void* res2, void* dx, void* pre, double* stats, void* stream) {
+                    const void* res2, void* dx, void* pre, double* stats, float* colsum, void* stream) {
   S3OD_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "conv_dgrad: channels %% 8");
   ConvGeo g0{}; g0.B = B; g0.SH = OH; g0.SW = OW; g0.SC = Cout; g0.KH = KH; g0.KW = KW; g0.s = stride; g0.p = pad;
   hipStream_t st = (hipStream_t)stream;
@@ -261,7 +270,7 @@ int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
             ConvDgradA<T, BM> la{}; la.dy = (const T*)dy; la.g = g; la.M = M;
             ConvDgradB<T, BN> lb{}; lb.w = (const T*)wp; lb.g = g; lb.NC = Cin;
             EpiStd<T, T> e{(T*)dx, (long)Cin, 0, bias, scale, shift, (const T*)res1, (long)Cin, (const T*)res2, (long)Cin,
-                           (T*)pre, (long)Cin, stats, act, M, N, rm};
+                           (T*)pre, (long)Cin, stats, act, M, N, rm, colsum};
             return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, cdiv(K, KT<T>::BK), 1, 1, st);
           });
         };
@@ -275,7 +284,8 @@ int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
 // conv wgrad: dw[Cout][Cin][KH][KW] (PyTorch layout, fp32) += sum_pix dy[pix][co] * x[src(pix,tap)][ci]
 // dy: [B,OH,OW,Cout]; x: [B,H,W,Cin].  Also serves ConvTranspose2d weights (conv view).
 int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW,
-                    int stride, int pad, const void* dy, const void* x, int relu_x, float* dw, int split, void* stream) {
+                    int stride, int pad, const void* dy, const void* x, int relu_x, float* dw, float* ws, int split,
+                    void* stream) {
   S3OD_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "conv_wgrad: channels %% 8");
   ConvGeo g{}; g.B = B; g.SH = H; g.SW = W; g.SC = Cin; g.RH = OH; g.RW = OW; g.KH = KH; g.KW = KW; g.s = stride; g.p = pad;
   const int NPIX = B * OH * OW, M = Cout, N = KH * KW * Cin;
@@ -288,8 +298,15 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
       if (sp <= 0) { int tiles = cdiv(M, BM) * cdiv(N, BN); sp = max(1, min(KTILES / 8, 2048 / max(tiles, 1))); }
       DenseMC<T, BM> la{(const T*)dy, (long)Cout, NPIX, Cout};
       WgradB<T, BN, decltype(rl)::value> lb{}; lb.x = (const T*)x; lb.g = g; lb.NPIX = NPIX; lb.relu = relu_x;
-      EpiWgrad e{dw, M, N, Cin, KH * KW};
-      return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, KTILES, sp, 1, st);
+      // taps > 1: the split-K atomics go to a workspace in the GEMM's own [Cout][tap][Cin] layout
+      // (a wave's adds hit contiguous addresses), then one pass permutes into the PyTorch layout
+      const bool viaws = ws != nullptr && KH * KW > 1;
+      if (viaws) (void)hipMemsetAsync(ws, 0, sizeof(float) * (size_t)M * N, st);
+      EpiWgrad e = viaws ? EpiWgrad{ws, M, N, N, 1} : EpiWgrad{dw, M, N, Cin, KH * KW};
+      int rc = launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, KTILES, sp, 1, st);
+      if (rc || !viaws) return rc;
+      hipLaunchKernelGGL(wgrad_permute_add_kernel, dim3(cdiv((long)M * N, 256)), dim3(256), 0, st, ws, dw, M, Cin, KH * KW);
+      return s3od_check_launch("conv_wgrad permute");
     };
     if (relu_x) {
       if (Cout <= 64) return go(std::integral_constant<int, 64>{}, std::true_type{});

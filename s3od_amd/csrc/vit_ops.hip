@@ -97,7 +97,7 @@ template <typename T>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, const float* __restrict__ x,
                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
                                                       const float* __restrict__ w, const float* __restrict__ dres,
-                                                      float* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db,
+                                                      float* __restrict__ dx, float* __restrict__ ws,
                                                       int M, int rows_per_block) {
   __shared__ float sdw[768], sdb[768];
   for (int i = threadIdx.x; i < 768; i += 256) { sdw[i] = 0.f; sdb[i] = 0.f; }
@@ -111,6 +111,10 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
     const float* xr = x + (long)row * 768;
     float mu = mean[row], rs = rstd[row];
     float xh[12], g[12], dyv[12];
+    float4 rr4[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)   // issue the residual-gradient loads before the row reductions
+      rr4[i] = dres ? *(const float4*)(dres + (long)row * 768 + 4 * (lane + 64 * i)) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int i = 0; i < 3; i++) {
       int c = 4 * (lane + 64 * i);
@@ -132,8 +136,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
     for (int i = 0; i < 3; i++) {
       int c = 4 * (lane + 64 * i);
       float o[4];
-      float4 r = dres ? *(const float4*)(dres + (long)row * 768 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-      float rr[4] = {r.x, r.y, r.z, r.w};
+      float rr[4] = {rr4[i].x, rr4[i].y, rr4[i].z, rr4[i].w};
 #pragma unroll
       for (int e = 0; e < 4; e++) {
         int k = 4 * i + e;
@@ -153,7 +156,17 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
       atomicAdd(&sdb[c], pb[4 * i + e]);
     }
   __syncthreads();
-  for (int i = threadIdx.x; i < 768; i += 256) { atomicAdd(dw + i, sdw[i]); atomicAdd(db + i, sdb[i]); }
+  float* rep = ws + (long)(blockIdx.x % S3OD_NREP) * 1536;   // replicated [dw | db] partials
+  for (int i = threadIdx.x; i < 768; i += 256) { atomicAdd(rep + i, sdw[i]); atomicAdd(rep + 768 + i, sdb[i]); }
+}
+
+// a[i] += sum_r ws[r][i], b[i] += sum_r ws[r][768 + i]   (fold of the replicated 2x768 partials)
+__global__ void fold768x2_kernel(const float* __restrict__ ws, float* __restrict__ a, float* __restrict__ b) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 1536) return;
+  float s = 0.f;
+  for (int r = 0; r < S3OD_NREP; r++) s += ws[r * 1536 + i];
+  if (i < 768) a[i] += s; else b[i - 768] += s;
 }
 
 // taps: x f32 [B, Ntok, 768] -> T [B, P, 768] (drop 1 + 4 prefix tokens; src/s3od/model.py:75-84)
@@ -212,16 +225,18 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ a, lo
 }
 
 // LayerScale backward: du = dx * lam (T); dlam[n] += sum_m dx*u ; dbias[n] += sum_m du
+// block = 384 threads = 96 column groups (8 columns) x 4 row phases; LDS reduction, 2x768 atomics per block
 template <typename T>
-__global__ void scale_bwd_kernel(const float* __restrict__ dx, const T* __restrict__ u, const float* __restrict__ lam,
-                                 T* __restrict__ du, float* __restrict__ dlam, float* __restrict__ dbias, int M, int rows_per_block) {
-  int n = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  if (n >= 768) return;
-  int r0 = blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
+__global__ void __launch_bounds__(384) scale_bwd_kernel(const float* __restrict__ dx, const T* __restrict__ u, const float* __restrict__ lam,
+                                 T* __restrict__ du, float* __restrict__ ws, int M, int rows_per_block) {
+  __shared__ float red[384 * 8];
+  const int t = threadIdx.x, g = t % 96, ph = t / 96;
+  const int n = g * 8;
+  int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
   float l[8]; load8<float>(lam + n, l);
   float sl[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll 4
-  for (int r = r0; r < r1; r++) {
+  for (int r = r0 + ph; r < r1; r += 4) {
     float d[8], uu[8], o[8];
     load8<float>(dx + (long)r * 768 + n, d);
     load8<T>(u + (long)r * 768 + n, uu);
@@ -229,49 +244,85 @@ __global__ void scale_bwd_kernel(const float* __restrict__ dx, const T* __restri
     for (int e = 0; e < 8; e++) { o[e] = d[e] * l[e]; sl[e] += d[e] * uu[e]; sb[e] += o[e]; }
     store8<T>(du + (long)r * 768 + n, o);
   }
+  for (int pass = 0; pass < 2; pass++) {
+    __syncthreads();
 #pragma unroll
-  for (int e = 0; e < 8; e++) { atomicAdd(dlam + n + e, sl[e]); atomicAdd(dbias + n + e, sb[e]); }
+    for (int e = 0; e < 8; e++) red[t * 8 + e] = pass ? sb[e] : sl[e];
+    __syncthreads();
+    for (int c = t; c < 768; c += 384) {
+      const int gg = c >> 3, e = c & 7;
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; q++) s += red[(q * 96 + gg) * 8 + e];
+      atomicAdd(ws + (long)(blockIdx.x % S3OD_NREP) * 1536 + (pass ? 768 : 0) + c, s);
+    }
+  }
 }
 
 // dq,dk,dv [B,H,N,64] (dq w.r.t. the 1/8-scaled, rotated q) -> dqkv [B*N, 2304] T w.r.t. the
 // pre-RoPE projections: d(pre) = cos*dy - R(sin*dy), R = rotate_half; dq additionally * 1/8.
+// Also accumulates the q / v bias gradients (column sums of dqkv; k_proj has no bias).
+// block = 288 threads = (which, head, 8-wide d chunk) x rows_per_block rows
 template <typename T>
-__global__ void qkv_unrope_kernel(const T* __restrict__ dq, const T* __restrict__ dk, const T* __restrict__ dv,
+__global__ void __launch_bounds__(288) qkv_unrope_kernel(const T* __restrict__ dq, const T* __restrict__ dk, const T* __restrict__ dv,
                                   const float* __restrict__ cs, const float* __restrict__ sn,
-                                  T* __restrict__ dqkv, int B, int Ntok, int P) {
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;   // (m, which, h, d8)
-  long total = (long)B * Ntok * 3 * 12 * 8;
-  if (idx >= total) return;
-  int d8 = idx % 8; long r = idx / 8;
-  int h = r % 12; r /= 12;
-  int which = r % 3; long m = r / 3;
-  int b = m / Ntok, t = m % Ntok;
+                                  T* __restrict__ dqkv, float* __restrict__ ws,
+                                  int B, int Ntok, int P, int rows_per_block) {
+  const int t = threadIdx.x;
+  const int d8 = t & 7, h = (t >> 3) % 12, which = t / 96;
+  const int d0 = d8 * 8;
+  const int pd = d0 < 32 ? d0 + 32 : d0 - 32;
   const T* src = which == 0 ? dq : (which == 1 ? dk : dv);
-  const T* row = src + (((long)b * 12 + h) * Ntok + t) * 64;
-  int d0 = d8 * 8;
-  float v[8];
-  load8<T>(row + d0, v);
-  if (which < 2 && t >= Ntok - P) {
-    int tp = t - (Ntok - P);
-    int pd = d0 < 32 ? d0 + 32 : d0 - 32;
-    float pv[8]; load8<T>(row + pd, pv);
-    const float* cr = cs + (long)tp * 64; const float* sr = sn + (long)tp * 64;
-    float o[8];
+  const long M = (long)B * Ntok;
+  const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  constexpr int RB = 4;   // rows whose loads are issued together
+  for (long m0 = r0; m0 < r1; m0 += RB) {
+    float v[RB][8], pv[RB][8], cr[RB][8], sr[RB][8];
+    bool rot[RB];
 #pragma unroll
-    for (int e = 0; e < 8; e++) {
-      int d = d0 + e, dp = pd + e;
-      // y = x*cos + R(x)*sin  =>  dx = cos*dy + R^T(sin*dy);  R^T(z)[d] = z[d+32] (d<32), -z[d-32] (d>=32)
-      float rt = d < 32 ? sr[dp] * pv[e] : -sr[dp] * pv[e];
-      o[e] = cr[d] * v[e] + rt;
+    for (int j = 0; j < RB; j++) {
+      const long m = min(m0 + j, r1 - 1);
+      const int b = m / Ntok, tk = m - (long)b * Ntok;
+      const T* row = src + (((long)b * 12 + h) * Ntok + tk) * 64;
+      const int tp = max(tk - (Ntok - P), 0);
+      rot[j] = which < 2 && tk >= Ntok - P;
+      load8<T>(row + d0, v[j]);
+      load8<T>(row + pd, pv[j]);
+      load8<float>(cs + (long)tp * 64 + d0, cr[j]);
+      load8<float>(sn + (long)tp * 64 + pd, sr[j]);
     }
 #pragma unroll
-    for (int e = 0; e < 8; e++) v[e] = o[e];
-  }
-  if (which == 0) {
+    for (int j = 0; j < RB; j++) {
+      const long m = m0 + j;
+      if (m >= r1) break;
+      float o[8];
 #pragma unroll
-    for (int e = 0; e < 8; e++) v[e] *= 0.125f;
+      for (int e = 0; e < 8; e++) {
+        // y = x*cos + R(x)*sin  =>  dx = cos*dy + R^T(sin*dy);  R^T(z)[d] = z[d+32] (d<32), -z[d-32] (d>=32)
+        float rt = d0 < 32 ? sr[j][e] * pv[j][e] : -sr[j][e] * pv[j][e];
+        o[e] = rot[j] ? cr[j][e] * v[j][e] + rt : v[j][e];
+        if (which == 0) o[e] *= 0.125f;
+        acc[e] += o[e];
+      }
+      store8<T>(dqkv + m * 2304 + which * 768 + h * 64 + d0, o);
+    }
   }
-  store8<T>(dqkv + m * 2304 + which * 768 + h * 64 + d0, v);
+  if (which != 1 && ws) {   // replicated partials: ws[blk % NREP][q 768 | v 768]
+    float* dst = ws + (long)(blockIdx.x % S3OD_NREP) * 1536 + (which == 0 ? 0 : 768) + h * 64 + d0;
+#pragma unroll
+    for (int e = 0; e < 8; e++) atomicAdd(dst + e, acc[e]);
+  }
+}
+
+// out_q[i] += sum_r ws[r][i], out_v[i] += sum_r ws[r][768 + i]
+__global__ void qv_bias_fold_kernel(const float* __restrict__ ws, float* __restrict__ dbq, float* __restrict__ dbv) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 1536) return;
+  float s = 0.f;
+  for (int r = 0; r < S3OD_NREP; r++) s += ws[r * 1536 + i];
+  if (i < 768) { if (dbq) dbq[i] += s; }
+  else if (dbv) dbv[i - 768] += s;
 }
 
 // d(cls) = sum_b dx[b,0], d(reg[t]) = sum_b dx[b,1+t]  (accumulate)
@@ -319,12 +370,16 @@ int s3od_layernorm_fwd(int dtype, const float* x, const float* w, const float* b
   return s3od_check_launch("layernorm_fwd");
 }
 
+// ws: workspace of S3OD_NREP * 1536 floats (replicated dw / db partials)
 int s3od_layernorm_bwd(int dtype, const void* dy, const float* x, const float* mean, const float* rstd, const float* w,
-                       const float* dres, float* dx, float* dw, float* db, int M, void* stream) {
+                       const float* dres, float* dx, float* dw, float* db, float* ws, int M, void* stream) {
   const int rpb = 64;
+  hipStream_t st = (hipStream_t)stream;
+  (void)hipMemsetAsync(ws, 0, sizeof(float) * S3OD_NREP * 1536, st);
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3(cdiv(M, rpb)), dim3(256), 0, (hipStream_t)stream, (const T*)dy, x, mean, rstd, w, dres, dx, dw, db, M, rpb);
+    hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3(cdiv(M, rpb)), dim3(256), 0, st, (const T*)dy, x, mean, rstd, w, dres, dx, ws, M, rpb);
   });
+  hipLaunchKernelGGL(fold768x2_kernel, dim3(6), dim3(256), 0, st, ws, dw, db);
   return s3od_check_launch("layernorm_bwd");
 }
 
@@ -347,23 +402,31 @@ int s3od_colsum(int dtype, const void* a, long lda, int M, int N, float* out, vo
   return s3od_check_launch("colsum");
 }
 
+// ws: workspace of S3OD_NREP * 1536 floats (replicated dlam / dbias partials)
 int s3od_layerscale_bwd(int dtype, const float* dx, const void* u, const float* lam, void* du, float* dlam, float* dbias,
-                        int M, void* stream) {
-  const int rpb = 128;
-  dim3 grid(1, cdiv(M, rpb));
+                        float* ws, int M, void* stream) {
+  const int rpb = 64;
+  hipStream_t st = (hipStream_t)stream;
+  (void)hipMemsetAsync(ws, 0, sizeof(float) * S3OD_NREP * 1536, st);
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(scale_bwd_kernel<T>, grid, dim3(96), 0, (hipStream_t)stream, dx, (const T*)u, lam, (T*)du, dlam, dbias, M, rpb);
+    hipLaunchKernelGGL(scale_bwd_kernel<T>, dim3(cdiv(M, rpb)), dim3(384), 0, st, dx, (const T*)u, lam, (T*)du, ws, M, rpb);
   });
+  hipLaunchKernelGGL(fold768x2_kernel, dim3(6), dim3(256), 0, st, ws, dlam, dbias);
   return s3od_check_launch("layerscale_bwd");
 }
 
 int s3od_qkv_unrope(int dtype, const void* dq, const void* dk, const void* dv, const float* cs, const float* sn,
-                    void* dqkv, int B, int Ntok, int P, void* stream) {
-  long total = (long)B * Ntok * 3 * 12 * 8;
+                    void* dqkv, float* dbq, float* dbv, float* ws, int B, int Ntok, int P, void* stream) {
+  S3OD_REQUIRE(ws || (!dbq && !dbv), "qkv_unrope: bias gradients need the workspace");
+  const long M = (long)B * Ntok;
+  const int rpb = dev_knob("S3OD_UNROPE_RPB", 64);
+  hipStream_t st = (hipStream_t)stream;
+  if (ws) (void)hipMemsetAsync(ws, 0, sizeof(float) * S3OD_NREP * 1536, st);
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(qkv_unrope_kernel<T>, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream,
-                       (const T*)dq, (const T*)dk, (const T*)dv, cs, sn, (T*)dqkv, B, Ntok, P);
+    hipLaunchKernelGGL(qkv_unrope_kernel<T>, dim3(cdiv(M, rpb)), dim3(288), 0, st, (const T*)dq, (const T*)dk,
+                       (const T*)dv, cs, sn, (T*)dqkv, ws, B, Ntok, P, rpb);
   });
+  if (ws) hipLaunchKernelGGL(qv_bias_fold_kernel, dim3(6), dim3(256), 0, st, ws, dbq, dbv);
   return s3od_check_launch("qkv_unrope");
 }
 

@@ -127,12 +127,12 @@ class DPTEngine:
               row_mode, P, prefix, stream())
 
     def _conv(self, x, w, B, H, W, Cin, Cout, k, s, p, bias=None, scale=None, shift=None, act=ACT_NONE,
-              relu_in=False, res1=None, res2=None, out=None, pre=None, stats=None):
+              relu_in=False, res1=None, res2=None, out=None, pre=None, stats=None, colsum=None):
         OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         if out is None:
             out = torch.empty((B, OH, OW, Cout), dtype=self.tdt, device=x.device)
         lib()("s3od_conv_fwd", self.dt, B, H, W, Cin, OH, OW, Cout, k, k, s, p, x, int(relu_in), w,
-              bias, scale, shift, act, res1, res2, out, pre, stats, stream())
+              bias, scale, shift, act, res1, res2, out, pre, stats, colsum, stream())
         return out
 
     def _convT(self, x, w, B, IH, IW, Cin_T, Cout_T, k, s, p, bias=None, act=ACT_NONE, out=None):
@@ -141,7 +141,7 @@ class DPTEngine:
         if out is None:
             out = torch.empty((B, OH, OW, Cout_T), dtype=self.tdt, device=x.device)
         lib()("s3od_conv_dgrad", self.dt, B, OH, OW, Cout_T, IH, IW, Cin_T, k, k, s, p, x, w,
-              bias, None, None, act, None, None, out, None, None, stream())
+              bias, None, None, act, None, None, out, None, None, None, stream())
         return out
 
     def _bilinear(self, x, B, IH, IW, OH, OW, C):
@@ -344,26 +344,29 @@ class DPTEngine:
     def _wgrad_lin(self, dy, x, Nout, Kin, rows, dw, lddy=None, ldx=None):
         lib()("s3od_linear_wgrad", self.dt, Nout, Kin, rows, dy, lddy or Nout, x, ldx or Kin, dw, 0, stream())
 
-    def _dgrad_lin(self, dy, w, M, N, K, out, act=ACT_NONE, aux=None, out_f32=False, row_mode=0, P=0, prefix=0, ldaux=None):
+    def _dgrad_lin(self, dy, w, M, N, K, out, act=ACT_NONE, aux=None, out_f32=False, row_mode=0, P=0, prefix=0, ldaux=None,
+                   colsum=None):
         lib()("s3od_linear_dgrad", self.dt, M, N, K, dy, K, w, act, aux, ldaux or N, out, N, int(out_f32),
-              row_mode, P, prefix, stream())
+              row_mode, P, prefix, colsum, stream())
 
     def _wgrad_conv(self, dy, x, B, H, W, Cin, OH, OW, Cout, k, s, p, dw, relu_x=False):
-        lib()("s3od_conv_wgrad", self.dt, B, H, W, Cin, OH, OW, Cout, k, k, s, p, dy, x, int(relu_x), dw, 0, stream())
+        # taps > 1: fp32 workspace in the GEMM's [Cout][tap][Cin] layout (contiguous split-K atomics)
+        ws = torch.empty(Cout * k * k * Cin, dtype=torch.float32, device=dy.device) if k > 1 else None
+        lib()("s3od_conv_wgrad", self.dt, B, H, W, Cin, OH, OW, Cout, k, k, s, p, dy, x, int(relu_x), dw, ws, 0, stream())
 
-    def _dgrad_conv(self, dy, w, B, H, W, Cin, OH, OW, Cout, k, s, p, act=ACT_NONE, res1=None, out=None):
-        """dx [B,H,W,Cin] of a conv whose output grid is OH x OW with Cout channels."""
+    def _dgrad_conv(self, dy, w, B, H, W, Cin, OH, OW, Cout, k, s, p, act=ACT_NONE, res1=None, out=None, colsum=None):
+        """dx [B,H,W,Cin] of a conv whose output grid is OH x OW with Cout channels (colsum: += column sums of dx)."""
         if out is None:
             out = torch.empty((B, H, W, Cin), dtype=self.tdt, device=dy.device)
         lib()("s3od_conv_dgrad", self.dt, B, H, W, Cin, OH, OW, Cout, k, k, s, p, dy, w, None, None, None, act, res1,
-              None, out, None, None, stream())
+              None, out, None, None, colsum, stream())
         return out
 
     def _dgrad_conv_res(self, dy, w, B, H, W, C, act, res1, res2):
         """3x3 s1 dgrad with RELU_BWD mask (res1 = the un-ReLU'd input) plus a residual gradient res2."""
         out = torch.empty((B, H, W, C), dtype=self.tdt, device=dy.device)
         lib()("s3od_conv_dgrad", self.dt, B, H, W, C, H, W, C, 3, 3, 1, 1, dy, w, None, None, None, act, res1,
-              res2, out, None, None, stream())
+              res2, out, None, None, None, stream())
         return out
 
     def _rcu_bwd(self, d_out, r, u, B, ctx, G):
@@ -376,17 +379,15 @@ class DPTEngine:
         h, w = c["h"], c["w"]
         npix = B * h * w
         dev = d_out.device
-        sums = torch.empty(512, dtype=torch.float64, device=dev)
+        sums = torch.empty(32 * 3 * 256, dtype=torch.float64, device=dev)   # S3OD_NREP replicas
         dz2 = torch.empty_like(d_out)
         L("s3od_bn_bwd", self.dt, d_out, c["z2"], None, c["bn2"]["mean"], c["bn2"]["rstd"], P[q + "bn2.weight"], sums, dz2,
-          G[q + "bn2.weight"], G[q + "bn2.bias"], npix, 256, st)
-        self._colsum(dz2, npix, 256, G[q + "conv2.bias"])
+          G[q + "bn2.weight"], G[q + "bn2.bias"], G[q + "conv2.bias"], npix, 256, st)
         self._wgrad_conv(dz2, c["a1"], B, h, w, 256, h, w, 256, 3, 1, 1, G[q + "conv2.weight"])
         da1 = self._dgrad_conv(dz2, W8[tag + ".c2"], B, h, w, 256, h, w, 256, 3, 1, 1)
         dz1 = torch.empty_like(d_out)
         L("s3od_bn_bwd", self.dt, da1, c["z1"], c["a1"], c["bn1"]["mean"], c["bn1"]["rstd"], P[q + "bn1.weight"], sums, dz1,
-          G[q + "bn1.weight"], G[q + "bn1.bias"], npix, 256, st)
-        self._colsum(dz1, npix, 256, G[q + "conv1.bias"])
+          G[q + "bn1.weight"], G[q + "bn1.bias"], G[q + "conv1.bias"], npix, 256, st)
         self._wgrad_conv(dz1, c["x"], B, h, w, 256, h, w, 256, 3, 1, 1, G[q + "conv1.weight"], relu_x=True)
         return self._dgrad_conv_res(dz1, W8[tag + ".c1"], B, h, w, 256, ACT_RELU_BWD, c["x"], d_out)
 
@@ -424,21 +425,20 @@ class DPTEngine:
         npx = B * HH * WW
         # ---- three mask heads
         dh = torch.empty((npx, 96), dtype=self.tdt, device=dev)
-        L("s3od_mask_heads_bwd", dt, d_logits.contiguous(), hd["hsave"], W8["heads2"], dh, G["heads2_w"], G["heads2_b"], B, HH * WW, st)
-        self._colsum(dh, npx, 96, G["heads1_b"])
+        L("s3od_mask_heads_bwd", dt, d_logits.contiguous(), hd["hsave"], W8["heads2"], dh, G["heads2_w"], G["heads2_b"],
+          G["heads1_b"], B, HH * WW, st)
         self._wgrad_conv(dh, c64, B, HH, WW, 64, HH, WW, 96, 3, 1, 1, G["heads1_w"])
-        d64 = self._dgrad_conv(dh, W8["heads1"], B, HH, WW, 64, HH, WW, 96, 3, 1, 1, act=ACT_RELU_BWD, res1=c64)
+        # (bias gradients are column sums fused into the epilogue that produces each gradient)
+        d64 = self._dgrad_conv(dh, W8["heads1"], B, HH, WW, 64, HH, WW, 96, 3, 1, 1, act=ACT_RELU_BWD, res1=c64,
+                               colsum=G[m + "upsample_2x.2.bias"])
         # ---- upsample_2x.2 conv 64->64 + ReLU
-        self._colsum(d64, npx, 64, G[m + "upsample_2x.2.bias"])
         self._wgrad_conv(d64, up, B, HH, WW, 64, HH, WW, 64, 3, 1, 1, G[m + "upsample_2x.2.weight"])
-        dup = self._dgrad_conv(d64, W8["c64"], B, HH, WW, 64, HH, WW, 64, 3, 1, 1, act=ACT_RELU_BWD, res1=up)
+        dup = self._dgrad_conv(d64, W8["c64"], B, HH, WW, 64, HH, WW, 64, 3, 1, 1, act=ACT_RELU_BWD, res1=up,
+                               colsum=G[m + "upsample_2x.0.bias"])
         # ---- upsample_2x.0 ConvTranspose 128->64 k4 s2 p1 + ReLU (conv view: Y=oc1 grid, X=up grid)
-        self._colsum(dup, npx, 64, G[m + "upsample_2x.0.bias"])
         self._wgrad_conv(oc1, dup, B, HH, WW, 64, H1, W1, 128, 4, 2, 1, G[m + "upsample_2x.0.weight"])
-        doc1 = self._conv(dup, W8["up2x"], B, HH, WW, 64, 128, 4, 2, 1)
+        doc1 = self._conv(dup, W8["up2x"], B, HH, WW, 64, 128, 4, 2, 1, colsum=G[m + "output_conv1.bias"])
         # ---- output_conv1 3x3 256->128
-        n1 = B * H1 * W1
-        self._colsum(doc1, n1, 128, G[m + "output_conv1.bias"])
         self._wgrad_conv(doc1, p1, B, H1, W1, 256, H1, W1, 128, 3, 1, 1, G[m + "output_conv1.weight"])
         dp1 = self._dgrad_conv(doc1, W8["oc1"], B, H1, W1, 256, H1, W1, 128, 3, 1, 1)
         # ---- classifier head -> broadcast gradient onto path_1 (folded into the bilinear backward)
@@ -455,29 +455,28 @@ class DPTEngine:
         feats, dims = dec["feats"], dec["dims"]
         drn = [drn1, drn2, drn3, drn4]
         dfeat = []
+        # the feature gradient's column sums: resize_layers.{0,1,3}.bias; feature 2 is projects.2's output
+        fbias = [h + "resize_layers.0.bias", h + "resize_layers.1.bias", h + "projects.2.bias", h + "resize_layers.3.bias"]
         for i, f in enumerate(feats):
             hh, ww = dims[i]
             C = f.shape[3]
             self._wgrad_conv(drn[i], f, B, hh, ww, C, hh, ww, 256, 3, 1, 1, G[h + f"scratch.layer{i + 1}_rn.weight"])
-            dfeat.append(self._dgrad_conv(drn[i], W8[f"rn{i + 1}"], B, hh, ww, C, hh, ww, 256, 3, 1, 1))
+            dfeat.append(self._dgrad_conv(drn[i], W8[f"rn{i + 1}"], B, hh, ww, C, hh, ww, 256, 3, 1, 1, colsum=G[fbias[i]]))
         proj = dec["proj"]
         dproj = [None] * 4
         # resize0: ConvT 256 k4 s4 (conv view: Y = proj0 grid, X = f0 grid)
-        self._colsum(dfeat[0], B * dims[0][0] * dims[0][1], 256, G[h + "resize_layers.0.bias"])
         self._wgrad_conv(proj[0], dfeat[0], B, dims[0][0], dims[0][1], 256, ph, pw, 256, 4, 4, 0, G[h + "resize_layers.0.weight"])
-        dproj[0] = self._conv(dfeat[0], W8["rs0"], B, dims[0][0], dims[0][1], 256, 256, 4, 4, 0)
-        self._colsum(dfeat[1], B * dims[1][0] * dims[1][1], 512, G[h + "resize_layers.1.bias"])
+        dproj[0] = self._conv(dfeat[0], W8["rs0"], B, dims[0][0], dims[0][1], 256, 256, 4, 4, 0, colsum=G[h + "projects.0.bias"])
         self._wgrad_conv(proj[1], dfeat[1], B, dims[1][0], dims[1][1], 512, ph, pw, 512, 2, 2, 0, G[h + "resize_layers.1.weight"])
-        dproj[1] = self._conv(dfeat[1], W8["rs1"], B, dims[1][0], dims[1][1], 512, 512, 2, 2, 0)
+        dproj[1] = self._conv(dfeat[1], W8["rs1"], B, dims[1][0], dims[1][1], 512, 512, 2, 2, 0, colsum=G[h + "projects.1.bias"])
         dproj[2] = dfeat[2]
-        self._colsum(dfeat[3], B * dims[3][0] * dims[3][1], 1024, G[h + "resize_layers.3.bias"])
         self._wgrad_conv(dfeat[3], proj[3], B, ph, pw, 1024, dims[3][0], dims[3][1], 1024, 3, 2, 1, G[h + "resize_layers.3.weight"])
-        dproj[3] = self._dgrad_conv(dfeat[3], W8["rs3"], B, ph, pw, 1024, dims[3][0], dims[3][1], 1024, 3, 2, 1)
+        dproj[3] = self._dgrad_conv(dfeat[3], W8["rs3"], B, ph, pw, 1024, dims[3][0], dims[3][1], 1024, 3, 2, 1,
+                                    colsum=G[h + "projects.3.bias"])
         # projects (1x1, bias) -> tap gradients
         NP = ph * pw
         dtaps = []
         for i, c in enumerate(OUT_CH):
-            self._colsum(dproj[i], B * NP, c, G[h + f"projects.{i}.bias"])
             self._wgrad_lin(dproj[i], dec["taps"][i], c, D_, B * NP, G[h + f"projects.{i}.weight"])
             dtaps.append((dproj[i], c))
         return dtaps
@@ -502,6 +501,8 @@ class DPTEngine:
         dk = torch.empty_like(dq)
         dv = torch.empty_like(dq)
         delta = _E(None, (B * H_, Nt), torch.float32, dev)
+        qv_ws = _E(None, (32 * 1536,), torch.float32, dev)      # S3OD_NREP replicas of the q/v bias partials
+        red_ws = _E(None, (32 * 1536,), torch.float32, dev)     # same, for LayerNorm / LayerScale parameter grads
         for i in reversed(range(LAST_LAYER)):
             if i + 1 in tap_of:
                 dp, c = dtaps[tap_of[i + 1]]
@@ -512,29 +513,28 @@ class DPTEngine:
             s = ctx.t[f"L{i}"]
             # ---- MLP half
             L("s3od_layerscale_bwd", dt, dx, s["u2"], P[p + "layer_scale2.lambda1"], du, G[p + "layer_scale2.lambda1"],
-              G[p + "mlp.down_proj.bias"], M, st)
+              G[p + "mlp.down_proj.bias"], red_ws, M, st)
             self._wgrad_lin(du, s["a"], D_, 3072, M, G[p + "mlp.down_proj.weight"])
-            self._dgrad_lin(du, W8[f"down{i}"], M, 3072, D_, dhp, act=ACT_GELU_BWD, aux=s["hpre"])
-            self._colsum(dhp, M, 3072, G[p + "mlp.up_proj.bias"])
+            self._dgrad_lin(du, W8[f"down{i}"], M, 3072, D_, dhp, act=ACT_GELU_BWD, aux=s["hpre"],
+                            colsum=G[p + "mlp.up_proj.bias"])
             self._wgrad_lin(dhp, s["h2"], 3072, D_, M, G[p + "mlp.up_proj.weight"])
             self._dgrad_lin(dhp, W8[f"up{i}"], M, D_, 3072, dh)
             L("s3od_layernorm_bwd", dt, dh, s["xm"], s["mean2"], s["rstd2"], P[p + "norm2.weight"], dx, dxm,
-              G[p + "norm2.weight"], G[p + "norm2.bias"], M, st)
+              G[p + "norm2.weight"], G[p + "norm2.bias"], red_ws, M, st)
             # ---- attention half
             L("s3od_layerscale_bwd", dt, dxm, s["u1"], P[p + "layer_scale1.lambda1"], du, G[p + "layer_scale1.lambda1"],
-              G[p + "attention.o_proj.bias"], M, st)
+              G[p + "attention.o_proj.bias"], red_ws, M, st)
             self._wgrad_lin(du, s["o"], D_, D_, M, G[p + "attention.o_proj.weight"])
             do = dh
             self._dgrad_lin(du, W8[f"o{i}"], M, D_, D_, do)
             L("s3od_attn_bwd", dt, s["q"], s["k"], s["v"], s["o"], do, s["lse"], delta, dq, dk, dv, B, H_, Nt, st)
-            L("s3od_qkv_unrope", dt, dq, dk, dv, ctx.t["cos"], ctx.t["sin"], dqkv, B, Nt, NP, st)
-            self._colsum(dqkv[:, :D_], M, D_, G[p + "attention.q_proj.bias"], lda=3 * D_)
-            self._colsum(dqkv[:, 2 * D_:], M, D_, G[p + "attention.v_proj.bias"], lda=3 * D_)
+            L("s3od_qkv_unrope", dt, dq, dk, dv, ctx.t["cos"], ctx.t["sin"], dqkv, G[p + "attention.q_proj.bias"],
+              G[p + "attention.v_proj.bias"], qv_ws, B, Nt, NP, st)
             self._wgrad_lin(dqkv, s["h1"], 3 * D_, D_, M, G[f"qkv_w{i}"])
             dh1 = dh
             self._dgrad_lin(dqkv, W8[f"qkv{i}"], M, D_, 3 * D_, dh1)
             L("s3od_layernorm_bwd", dt, dh1, s["x"], s["mean1"], s["rstd1"], P[p + "norm1.weight"], dxm, dxi,
-              G[p + "norm1.weight"], G[p + "norm1.bias"], M, st)
+              G[p + "norm1.weight"], G[p + "norm1.bias"], red_ws, M, st)
             dx, dxi = dxi, dx
             if self.grad_hook is not None:
                 self.grad_hook(f"layer{i}")

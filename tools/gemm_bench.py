@@ -37,7 +37,7 @@ def dgrad(M, N, K):
     dy = torch.randn(M, K, device="cuda").bfloat16()
     w = torch.randn(K, N, device="cuda").bfloat16()
     o = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    f = lambda: lib()("s3od_linear_dgrad", BF16, M, N, K, dy, K, w, 0, None, N, o, N, 0, 0, 0, 0, stream())
+    f = lambda: lib()("s3od_linear_dgrad", BF16, M, N, K, dy, K, w, 0, None, N, o, N, 0, 0, 0, 0, None, stream())
     t = timeit(f)
     print(f"linear dgrad M={M} N={N} K={K}: {t * 1e6:8.1f} us  {2 * M * N * K / t / 1e12:7.1f} TF/s")
 
@@ -56,7 +56,7 @@ def conv(B, H, W, Cin, Cout, k=3):
     w = torch.randn(Cout, k, k, Cin, device="cuda").bfloat16()
     o = torch.empty(B, H, W, Cout, device="cuda", dtype=torch.bfloat16)
     f = lambda: lib()("s3od_conv_fwd", BF16, B, H, W, Cin, H, W, Cout, k, k, 1, k // 2, x, 0, w, None, None, None, 0, None,
-                      None, o, None, None, stream())
+                      None, o, None, None, None, stream())
     t = timeit(f, 10)
     fl = 2 * B * H * W * Cin * Cout * k * k
     print(f"conv fwd B={B} {H}x{W} {Cin}->{Cout} k{k}: {t * 1e6:8.1f} us  {fl / t / 1e12:7.1f} TF/s")
