@@ -89,6 +89,27 @@ def cpu_baseline(S, mode, threads):
                                       f"fp32 oracle (oracle/s3od_oracle.py), {n} timed iter after 1 warm-up, {threads} threads"}
 
 
+def infer_rate(model, B, S, steps, warmup, dev):
+    """Eval-forward throughput (configs[1] / configs[4]): one selected mask per image -> masks/s."""
+    x, _ = synthetic_batch(B, S, 7, dev)
+    was_training = model.training
+    model.eval()
+    with torch.no_grad():
+        for _ in range(warmup):
+            model(x)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = model(x)["pred_masks"]
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    model.train(was_training)
+    ok = bool(torch.isfinite(out).all().item())
+    del out, x
+    return {"value": round(B * steps / dt, 3), "unit": "masks/s", "ms_per_step": round(dt / steps * 1e3, 3),
+            "batch": B, "image_size": S, "steps": steps, "warmup": warmup, "finite": ok}
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/<tag>_pmc.json, written by tools/collect_profiles.py), or None."""
@@ -114,12 +135,16 @@ def main():
     ap.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-infer", action="store_true", help="skip the secondary inference lines (train mode)")
+    ap.add_argument("--ddp", action="store_true",
+                    help="use the RCCL data-parallel path even at world size 1 (rehearsal on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    use_dist = world > 1 or args.ddp
+    if use_dist:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
@@ -134,7 +159,7 @@ def main():
     S = args.size
     model = DPTSegmentation(compute_dtype=args.dtype).to(dev)
     sync = None
-    if world > 1:
+    if use_dist:
         from s3od_amd.ddp import GradSync, broadcast_parameters
         broadcast_parameters(model)
         sync = GradSync(model)
@@ -165,17 +190,17 @@ def main():
     dom = "s3od_attn_fwd"
     lib = _lib.lib()
     lib.timers = {dom: []}
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         last = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     el = time.perf_counter() - t0
-    if world > 1:
+    if use_dist:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
@@ -209,13 +234,19 @@ def main():
                          "flops_per_launch": attn_flops(B, S), "mean_launch_ms": round(kms, 4), "launches": len(ev)},
             "finite": ok,
         }
+        if args.mode == "train" and world == 1 and not args.no_infer and args.dtype == "bf16":
+            # the metric's second half ("infer masks/sec 1GPU"): configs[1] and configs[4]
+            res["infer"] = dict(infer_rate(model, 8, 1024, 10, 3, dev),
+                                config="dinob inference bs=8 1024x1024 eval forward (configs[1])")
+            res["infer_2048"] = dict(infer_rate(model, 4, 2048, 4, 2, dev),
+                                     config="high-res 2048x2048 eval forward bs=4 (configs[4])")
         if not args.no_cpu_baseline and world == 1:
             try:
                 res["cpu_baseline"] = cpu_baseline(S, args.mode, args.cpu_threads)
             except Exception as e:  # reported, never fatal for the GPU number
                 res["cpu_baseline"] = {"value": None, "error": repr(e)[:200]}
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

@@ -532,16 +532,20 @@ template <> struct Mma<float> {
 };
 
 // ------------------------------------------------------------------ the kernel
-template <typename T, int BM, int BN, int NST_ = 3> struct GemmShape {
+template <typename T, int BM, int BN, int NST_ = 3, int WM_ = 0> struct GemmShape {
   static constexpr int BK = KT<T>::BK;
   static constexpr int ABYTES = BM * 128, BBYTES = BN * 128;
   static constexpr int STAGE = ABYTES + BBYTES;
   static constexpr int NST = NST_;
   static constexpr int LDT = BN + 4;                       // fp32 C-tile row stride
-  static constexpr int CBYTES = BM * LDT * 4;
+  // the fp32 C tile is staged through LDS in row chunks of CROWS (half the tile when the whole
+  // tile would not fit beside the K stages, e.g. 256x256)
+  static constexpr int CROWS = (BM * LDT * 4 <= NST * STAGE || BM * LDT * 4 <= 160 * 1024) ? BM : BM / 2;
+  static constexpr int CBYTES = CROWS * LDT * 4;
   static constexpr int LDS = (NST * STAGE > CBYTES ? NST * STAGE : CBYTES);
+  static_assert(LDS <= 160 * 1024, "LDS budget");
   // wave grid: 8 waves as WM x WN
-  static constexpr int WM = BM >= 2 * BN ? 4 : (BN >= 2 * BM ? 2 : (BM >= BN ? 4 : 2));
+  static constexpr int WM = WM_ ? WM_ : (BM >= 2 * BN ? 4 : (BN >= 2 * BM ? 2 : (BM >= BN ? 4 : 2)));
   static constexpr int WN = GEMM_WAVES / WM;
   static constexpr int TM = BM / WM, TN = BN / WN;         // per-wave tile
   static constexpr int MI = TM / 16, NI = TN / 16;
@@ -552,6 +556,8 @@ struct KRange { int kt0, kt1; };
 
 template <int N> DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 DEV void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// workgroup barrier that orders LDS only (does not drain in-flight global loads / LDS-DMA)
+DEV void lds_barrier() { wait_lgkm0(); __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); }
 
 // Block-level epilogue contract:  epi(tile, LDT, m0, n0, tid, BM, BN)
 //
@@ -656,24 +662,208 @@ __global__ void __launch_bounds__(GEMM_THREADS) igemm_kernel(LA la, LB lb, EPI e
     }
   }
   __syncthreads();
-  // stage C tile to LDS (fp32)
+  // stage the C tile to LDS (fp32) in row chunks of CROWS and hand each chunk to the epilogue
   float* ct = (float*)smem;
 #pragma unroll
-  for (int i = 0; i < MI; i++)
+  for (int c0 = 0; c0 < BM; c0 += S::CROWS) {
+    if (c0) __syncthreads();
 #pragma unroll
-    for (int j = 0; j < NI; j++) {
-      int r = wm * S::TM + i * 16 + (lane >> 4) * 4;
-      int c = wn * S::TN + j * 16 + (lane & 15);
+    for (int i = 0; i < MI; i++) {
+      const int rb = wm * S::TM + i * 16;                    // wave-uniform
+      if (rb < c0 || rb >= c0 + S::CROWS) continue;
 #pragma unroll
-      for (int e = 0; e < 4; e++) ct[(r + e) * S::LDT + c] = acc[i][j][e];
+      for (int j = 0; j < NI; j++) {
+        int r = rb - c0 + (lane >> 4) * 4;
+        int c = wn * S::TN + j * 16 + (lane & 15);
+#pragma unroll
+        for (int e = 0; e < 4; e++) ct[(r + e) * S::LDT + c] = acc[i][j][e];
+      }
     }
-  __syncthreads();
-  epi(ct, S::LDT, m0, n0, tid, BM, BN);
+    __syncthreads();
+    epi(ct, S::LDT, m0 + c0, n0, tid, S::CROWS, BN);
+  }
 }
 
-// iterate 8-wide row segments of the staged tile: f(m, n, const float* v8)
+// ------------------------------------------------------------------ persistent variant
+// One workgroup per CU walks a list of output tiles (XCD-aware: the tiles of one XCD form a
+// contiguous row-major range, so its 32 CUs share A row panels and B in their L2).  The K-tile
+// stream runs ACROSS tiles: during the last K tile of tile i the loaders are re-pointed at tile
+// i+1 and its first K tile is DMA'd into the free stage, so that load and the epilogue of tile i
+// (C staged in 64-row chunks, stores left in flight) overlap instead of running back to back.
+// LDS: two K stages and a C-chunk region that aliases the stage just consumed:
+//   stage 0 = [0, STG), stage 1 = [STG+SLACK, 2*STG+SLACK); C region of stage 0 = [0, CB),
+//   of stage 1 = [STG, STG+CB)  (CB = STG+SLACK)  -> a C region never overlaps the other stage.
+// Wave grid 2 x 4 (per-wave 128 x 64): a 64-row C chunk is written by four waves.
+template <typename T, int BM, int BN> struct PShape {
+  typedef GemmShape<T, BM, BN, 2, 2> G;
+  static constexpr int CR = 64;
+  static constexpr int CB = CR * G::LDT * 4;
+  static constexpr int STG = G::STAGE;
+  static constexpr int SLACK = CB > STG ? CB - STG : 0;
+  static constexpr int LDS = 2 * STG + SLACK;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  static_assert(BM % CR == 0 && G::TM % 16 == 0, "chunking");
+};
+
+template <typename T, int BM, int BN, class LA, class LB, class EPI>
+__global__ void __launch_bounds__(GEMM_THREADS) pgemm_kernel(LA la, LB lb, EPI epi, int KTILES, int split, int tiles_x, int tiles_y) {
+  typedef PShape<T, BM, BN> P;
+  typedef typename P::G S;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int wm = wave / S::WN, wn = wave % S::WN;
+  constexpr int MI = S::MI, NI = S::NI, KS = Mma<T>::KSTEPS;
+  const int ntiles = tiles_x * tiles_y * split;
+  // ---- this workgroup's tile list (WG b runs on XCD b & 7)
+  const int G = gridDim.x, b = blockIdx.x, x = b & 7, j = b >> 3;
+  const int ng = (G - x + 7) >> 3;                           // WGs on XCD x
+  int cum = 0;
+  for (int y = 0; y < x; y++) cum += (G - y + 7) >> 3;
+  const int lo = (int)((long)ntiles * cum / G), hi = (int)((long)ntiles * (cum + ng) / G);
+  int tile = lo + j;
+  if (tile >= hi) return;
+  const int per = (KTILES + split - 1) / split;
+  auto coords = [&](int tl, int& m0, int& n0, int& kt0, int& kt1) {
+    const int xy = tiles_x * tiles_y, z = tl / xy, r = tl - z * xy, by = r / tiles_x;
+    m0 = by * BM; n0 = (r - by * tiles_x) * BN;
+    kt0 = z * per; kt1 = min(KTILES, kt0 + per);
+  };
+  auto stage = [&](int st) -> char* { return smem + (st ? P::STG + P::SLACK : 0); };
+  auto cregion = [&](int st) -> float* { return (float*)(smem + (st ? P::STG : 0)); };
+
+  f32x4 acc[MI][NI];
+  typedef typename Mma<T>::frag frag;
+  frag fa[2][MI], fb[2][NI];
+  auto read_frags = [&](int buf, const char* stg, int kk) {
+    const char* As = stg;
+    const char* Bs = stg + S::ABYTES;
+#pragma unroll
+    for (int i = 0; i < MI; i++) fa[buf][i] = Frag<T, LA::KCL, BM>::read(As, wm * S::TM + i * 16, kk, lane);
+#pragma unroll
+    for (int q = 0; q < NI; q++) fb[buf][q] = Frag<T, LB::KCL, BN>::read(Bs, wn * S::TN + q * 16, kk, lane);
+  };
+  auto mfmas = [&](int buf) {
+    if constexpr (LA::RELU) {
+#pragma unroll
+      for (int i = 0; i < MI; i++) fa[buf][i] = relu_frag(fa[buf][i]);
+    }
+    if constexpr (LB::RELU) {
+#pragma unroll
+      for (int q = 0; q < NI; q++) fb[buf][q] = relu_frag(fb[buf][q]);
+    }
+#pragma unroll
+    for (int i = 0; i < MI; i++)
+#pragma unroll
+      for (int q = 0; q < NI; q++) acc[i][q] = Mma<T>::mma(fa[buf][i], fb[buf][q], acc[i][q]);
+  };
+
+  int m0, n0, kt0, kt1;
+  coords(tile, m0, n0, kt0, kt1);
+  la.setup(m0, tid);
+  lb.setup(n0, tid);
+  int cur = 0;
+  if (kt1 > kt0) { la.issue(kt0, stage(0)); lb.issue(kt0, stage(0) + S::ABYTES); }
+  while (true) {
+    const int nt = kt1 - kt0;
+    const int next = tile + ng;
+    const bool has_next = next < hi;
+    int nm0 = 0, nn0 = 0, nkt0 = 0, nkt1 = 0;
+    if (has_next) coords(next, nm0, nn0, nkt0, nkt1);
+#pragma unroll
+    for (int i = 0; i < MI; i++)
+#pragma unroll
+      for (int q = 0; q < NI; q++) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (nt > 0) {
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      read_frags(0, stage(cur), 0);
+    }
+    for (int t = 0; t < nt; ++t) {
+      const bool pre = t + 1 < nt;
+      char* nx = stage(cur ^ 1);
+      if (pre) {
+        la.issue(kt0 + t + 1, nx);
+        lb.issue(kt0 + t + 1, nx + S::ABYTES);
+      } else if (has_next && nkt1 > nkt0) {
+        // last K tile of this tile: re-point the loaders and start the next tile's first K tile
+        la.setup(nm0, tid);
+        lb.setup(nn0, tid);
+        la.issue(nkt0, nx);
+        lb.issue(nkt0, nx + S::ABYTES);
+      }
+      const char* stg = stage(cur);
+#pragma unroll
+      for (int kk = 0; kk < KS; kk++) {
+        const int bb = kk & 1;
+        if (kk + 1 < KS) {
+          read_frags(bb ^ 1, stg, kk + 1);
+        } else if (pre) {
+          wait_vmcnt<0>();
+          wait_lgkm0();
+          __builtin_amdgcn_s_barrier();
+          read_frags(bb ^ 1, nx, 0);
+        }
+        mfmas(bb);
+      }
+      if (pre) cur ^= 1;
+    }
+    if (nt == 0 && has_next && nkt1 > nkt0) {      // empty split-K range: still start the next tile
+      la.setup(nm0, tid);
+      lb.setup(nn0, tid);
+      la.issue(nkt0, stage(cur ^ 1));
+      lb.issue(nkt0, stage(cur ^ 1) + S::ABYTES);
+    }
+    // ---- epilogue of this tile: C chunks in the region of the stage just consumed.  Raw barriers
+    // (LDS waits only): __syncthreads() would also drain the next tile's K-tile DMA.
+    lds_barrier();
+    float* ct = cregion(cur);
+#pragma unroll
+    for (int c0 = 0; c0 < BM; c0 += P::CR) {
+      if (c0) lds_barrier();
+#pragma unroll
+      for (int i = 0; i < MI; i++) {
+        const int rb = wm * S::TM + i * 16;                  // wave-uniform
+        if (rb < c0 || rb >= c0 + P::CR) continue;
+#pragma unroll
+        for (int q = 0; q < NI; q++) {
+          int r = rb - c0 + (lane >> 4) * 4;
+          int c = wn * S::TN + q * 16 + (lane & 15);
+#pragma unroll
+          for (int e = 0; e < 4; e++) ct[(r + e) * S::LDT + c] = acc[i][q][e];
+        }
+      }
+      lds_barrier();
+      epi(ct, S::LDT, m0 + c0, n0, tid, P::CR, BN);
+    }
+    if (!has_next) break;
+    lds_barrier();                                           // C region free before it is re-filled
+    tile = next; m0 = nm0; n0 = nn0; kt0 = nkt0; kt1 = nkt1;
+    cur ^= 1;
+  }
+}
+
+// iterate 8-wide row segments of the staged tile: f(m, n, const float* v8, r, c).  When the
+// thread count is a multiple of the segments per row (every config but the N=96 head), a thread
+// keeps ONE column group and the loop has a compile-time trip count, so it unrolls and the LDS
+// reads / global stores of all rows are in flight together.
 template <class F> DEV void for_segments(const float* ct, int LDT, int BM, int BN, int m0, int n0, int M, int N, int tid, F f) {
-  const int segs = BM * BN / 8, spr = BN / 8;
+  const int spr = BN / 8;
+  if (GEMM_THREADS % spr == 0 && BM % (GEMM_THREADS / spr) == 0) {
+    const int rpi = GEMM_THREADS / spr, cs = tid % spr, r0 = tid / spr;
+    const int n = n0 + cs * 8;
+    if (n >= N) return;
+#pragma unroll
+    for (int it = 0; it < BM / rpi; it++) {
+      const int r = r0 + it * rpi, m = m0 + r;
+      if (m >= M) break;
+      const float4* src = (const float4*)(ct + r * LDT + cs * 8);
+      float4 x0 = src[0], x1 = src[1];
+      float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      f(m, n, v, r, cs * 8);
+    }
+    return;
+  }
+  const int segs = BM * BN / 8;
   for (int s = tid; s < segs; s += GEMM_THREADS) {
     int r = s / spr, cs = s - r * spr;
     int m = m0 + r, n = n0 + cs * 8;
@@ -702,11 +892,29 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
     // a thread always sees the same 8-column group (GEMM_THREADS % (BN/8) == 0), so its column
     // partial sums live in registers until the block reduction below
     float cs8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // per-column affine terms of this thread's (fixed) 8-column group, loaded once
+    float b8[8], s8[8], h8[8];
+    {
+      const int nn = n0 + (tid % (BN / 8)) * 8;
+      const bool ok = nn < N;
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        b8[e] = (bias && ok) ? bias[nn + e] : 0.f;
+        s8[e] = (scale && ok) ? scale[nn + e] : 1.f;
+        h8[e] = (shift && ok) ? shift[nn + e] : 0.f;
+      }
+    }
+    const bool fixed_cols = GEMM_THREADS % (BN / 8) == 0;
     for_segments(ct, LDT, BM, BN, m0, n0, M, N, tid, [&](int m, int n, const float* a, int, int) {
       float pv[8], v[8], o[8];
       long orow = rm.map(m);
+      if (fixed_cols) {
 #pragma unroll
-      for (int e = 0; e < 8; e++) { pv[e] = a[e] + (bias ? bias[n + e] : 0.f); v[e] = pv[e] * (scale ? scale[n + e] : 1.f) + (shift ? shift[n + e] : 0.f); }
+        for (int e = 0; e < 8; e++) { pv[e] = a[e] + b8[e]; v[e] = pv[e] * s8[e] + h8[e]; }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; e++) { pv[e] = a[e] + (bias ? bias[n + e] : 0.f); v[e] = pv[e] * (scale ? scale[n + e] : 1.f) + (shift ? shift[n + e] : 0.f); }
+      }
       if (pre) store8<TP>(pre + orow * ldp + n, pv);
       if (act >= ACT_GELU_BWD) {
         float r[8]; load8<TR>(res1 + orow * ldr1 + n, r);
@@ -781,17 +989,30 @@ struct EpiWgrad {
   }
 };
 
+// NST = 0 selects the persistent two-stage kernel (pgemm_kernel, one workgroup per CU).
 template <typename T, int BM, int BN, class LA, class LB, class EPI, int NST = 3>
 static int launch_igemm(LA la, LB lb, EPI epi, int M, int N, int KTILES, int split, int zdim_extra, hipStream_t st) {
-  typedef GemmShape<T, BM, BN, NST> S;
   if (!la.buf_ok() || !lb.buf_ok()) {
     s3od_set_error("igemm: operand too large for a buffer descriptor or gather channels < %d", KT<T>::BK);
     return 22;
   }
+  if constexpr (NST == 0) {
+    typedef PShape<T, BM, BN> P;
+    auto kfn = pgemm_kernel<T, BM, BN, LA, LB, EPI>;
+    static bool attr = false;
+    if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, P::LDS); attr = true; }
+    const int tx = cdiv(N, BN), ty = cdiv(M, BM);
+    const long ntiles = (long)tx * ty * split * zdim_extra;
+    const int grid = (int)(ntiles < 256 ? ntiles : 256);
+    hipLaunchKernelGGL(kfn, dim3(grid), dim3(GEMM_THREADS), P::LDS, st, la, lb, epi, KTILES, split, tx, ty);
+    return s3od_check_launch("pgemm");
+  } else {
+  typedef GemmShape<T, BM, BN, NST> S;
   auto kfn = igemm_kernel<T, BM, BN, NST, LA, LB, EPI>;
   static bool attr = false;
   if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS); attr = true; }
   dim3 grid(cdiv(N, BN), cdiv(M, BM), split * zdim_extra);
   hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), S::LDS, st, la, lb, epi, KTILES, split);
   return s3od_check_launch("igemm");
+  }
 }

@@ -15,6 +15,8 @@ static RowMap dense_rm() { RowMap r{}; r.mode = 0; return r; }
 // every GEMM entry point; default (-1) = per-op choice below.
 //   0: 256x128, 3 stages (1 WG/CU)   1: 128x128, 2 stages (2 WG/CU)   2: 128x128, 3 stages
 //   3: 256x128, 2 stages (BN is clamped to 64 for 64-channel convs: 256x64 x 2 stages = 80 KB)
+//   4: 256x256, 2 stages (1 WG/CU, per-wave 64x128; C staged in two 128-row halves)
+//   5: 256x256 persistent (pgemm_kernel: 1 WG/CU walks tiles, next tile's loads overlap the epilogue)
 #include <stdlib.h>
 static int gemm_cfg() {
   static int c = -2;
@@ -29,6 +31,8 @@ template <class F> static int with_cfg(int def, F f) {
     case 1: return f(TileCfg<128, 128, 2>{});
     case 2: return f(TileCfg<128, 128, 3>{});
     case 3: return f(TileCfg<256, 128, 2>{});
+    case 4: return f(TileCfg<256, 256, 2>{});
+    case 5: return f(TileCfg<256, 256, 0>{});
     default: return f(TileCfg<256, 128, 3>{});
   }
 }
@@ -41,23 +45,36 @@ template <typename T> struct EpiQKV {
   int M, Ntok, P, H;
   DEV void prepare(int) {}
   DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN) const {
+    // this thread's fixed 8-column group: bias of its columns and of their RoPE partners (d +- 32)
+    float b8[8], bp8[8];
+    {
+      const int nn = n0 + (tid % (BN / 8)) * 8, dd = nn & 63, dc = dd < 32 ? 32 : -32;
+#pragma unroll
+      for (int e = 0; e < 8; e++) { b8[e] = bias ? bias[nn + e] : 0.f; bp8[e] = bias ? bias[nn + dc + e] : 0.f; }
+    }
+    const bool fixed_cols = GEMM_THREADS % (BN / 8) == 0;
     for_segments(ct, LDT, BM, BN, m0, n0, M, 3 * H * 64, tid, [&](int m, int n, const float* a, int r, int c) {
       int which = n / (H * 64), nn = n - which * H * 64, h = nn >> 6, d0 = nn & 63;
       int b = m / Ntok, t = m - b * Ntok;
       float val[8];
 #pragma unroll
-      for (int e = 0; e < 8; e++) val[e] = a[e] + (bias ? bias[n + e] : 0.f);
+      for (int e = 0; e < 8; e++) val[e] = a[e] + (fixed_cols ? b8[e] : (bias ? bias[n + e] : 0.f));
       if (which < 2 && t >= Ntok - P) {
         int dc = d0 < 32 ? 32 : -32;
-        const float* pa = ct + r * LDT + c + dc;
+        const float4* pa = (const float4*)(ct + r * LDT + c + dc);
+        float4 p0 = pa[0], p1 = pa[1];
+        float pv[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
         int tp = t - (Ntok - P);
-        const float* cr = cs + (long)tp * 64 + d0;
-        const float* sr = sn + (long)tp * 64 + d0;
+        const float4* cr = (const float4*)(cs + (long)tp * 64 + d0);
+        const float4* sr = (const float4*)(sn + (long)tp * 64 + d0);
+        float4 c0 = cr[0], c1 = cr[1], s0 = sr[0], s1 = sr[1];
+        float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
         for (int e = 0; e < 8; e++) {
-          float pv = pa[e] + (bias ? bias[n + dc + e] : 0.f);
-          float rot = d0 < 32 ? -pv : pv;
-          val[e] = val[e] * cr[e] + rot * sr[e];
+          float q = pv[e] + (fixed_cols ? bp8[e] : (bias ? bias[n + dc + e] : 0.f));
+          float rot = d0 < 32 ? -q : q;
+          val[e] = val[e] * cv[e] + rot * sv[e];
         }
       }
       if (which == 0) {
@@ -78,25 +95,37 @@ template <typename T> struct EpiHeads {
   int M, HW;
   DEV void prepare(int) {}
   DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN) const {
-    float* t = (float*)ct;  // relu in place
-    for (int s = tid; s < BM * 96; s += GEMM_THREADS) {
-      int r = s / 96, c = s - r * 96;
-      t[r * LDT + c] = fmaxf(t[r * LDT + c] + b1[c], 0.f);
-    }
-    __syncthreads();
+    // h = relu(acc + b1) is formed on the fly from the staged fp32 tile (no in-place pass)
     if (hsave) {
-      for_segments(ct, LDT, BM, 96, m0, 0, M, 96, tid, [&](int m, int n, const float* a, int, int) {
-        store8<T>(hsave + (long)m * 96 + n, a);
-      });
+      const int segs = BM * 12;                               // 12 segments of 8 channels per row
+      for (int s = tid; s < segs; s += GEMM_THREADS) {
+        int r = s / 12, c = (s - r * 12) * 8, m = m0 + r;
+        if (m >= M) continue;
+        const float4* src = (const float4*)(ct + r * LDT + c);
+        float4 x0 = src[0], x1 = src[1];
+        float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int e = 0; e < 8; e++) v[e] = fmaxf(v[e] + b1[c + e], 0.f);
+        store8<T>(hsave + (long)m * 96 + c, v);
+      }
     }
+    // logit_k = b2[k] + sum_j relu(acc[32k + j] + b1[32k + j]) * w2[32k + j]; k is wave-uniform
     for (int s = tid; s < 3 * BM; s += GEMM_THREADS) {
       int k = s / BM, r = s - k * BM;
       int m = m0 + r;
       if (m >= M) continue;
-      const float* row = ct + r * LDT + 32 * k;
+      const float4* row = (const float4*)(ct + r * LDT + 32 * k);
+      const float* bb = b1 + 32 * k;
+      const float* ww = w2 + 32 * k;
       float acc = b2[k];
-#pragma unroll 8
-      for (int j = 0; j < 32; j++) acc += row[j] * w2[k * 32 + j];
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        float4 x = row[q];
+        acc += fmaxf(x.x + bb[4 * q + 0], 0.f) * ww[4 * q + 0];
+        acc += fmaxf(x.y + bb[4 * q + 1], 0.f) * ww[4 * q + 1];
+        acc += fmaxf(x.z + bb[4 * q + 2], 0.f) * ww[4 * q + 2];
+        acc += fmaxf(x.w + bb[4 * q + 3], 0.f) * ww[4 * q + 3];
+      }
       int b = m / HW, pix = m - b * HW;
       logits[((long)b * 3 + k) * HW + pix] = acc;
     }
@@ -104,6 +133,24 @@ template <typename T> struct EpiHeads {
 };
 
 template <int BM, int BN> struct Tile {};
+
+// split-K factor of a wgrad GEMM from a time model: ceil(tiles*sp / slots) rounds of ceil(KT/sp)
+// K tiles each, plus the split-K fp32 atomics at the chip-wide atomic rate (~1.3 TB/s, guide
+// "Global float atomics").  slots = resident workgroups (256 CUs x WGs per CU by LDS).
+template <typename T, int BM, int BN, int NST> static int wgrad_split(int tiles, int KT) {
+  typedef GemmShape<T, BM, BN, NST> S;
+  const int per_cu = (160 * 1024) / S::LDS > 0 ? (160 * 1024) / S::LDS : 1;
+  const long slots = 256L * per_cu;
+  const double ck = 2.0 * BM * BN * S::BK / (3.9e6 / per_cu);      // us per K tile per WG
+  const double atom = (double)BM * BN * 4 / 1.3e6;                 // us of chip atomics per WG
+  int best = 1; double bt = 1e30;
+  for (int sp = 1; sp <= (KT >= 8 ? KT / 4 : 1); sp++) {
+    long wgs = (long)tiles * sp;
+    double t = (double)((wgs + slots - 1) / slots) * ((KT + sp - 1) / sp) * ck + wgs * atom;
+    if (t < bt * 0.999) { bt = t; best = sp; }
+  }
+  return best;
+}
 
 // dw[(co*Cin + ci)*taps + tap] += ws[(co*taps + tap)*Cin + ci]   (one thread per dw element)
 __global__ void wgrad_permute_add_kernel(const float* __restrict__ ws, float* __restrict__ dw, int Cout, int Cin, int taps) {
@@ -138,6 +185,8 @@ int s3od_linear_fwd(int dtype, int M, int N, int K, const void* x, long ldx, con
         DenseKC<T, BN> lb{(const T*)w, (long)K, N, K, 0};
         EpiStd<TO, TR, T> e{(TO*)out, ldo, 0, bias, scale, shift, (const TR*)res1, ldr1, (const TR*)res2, ldr2,
                             (T*)pre, ldp, nullptr, act, M, N, rm};
+        static const int epi_probe = dev_knob("S3OD_EPI_PROBE", 0);   // dev: 1 = skip the epilogue's stores
+        if (epi_probe == 1) e.M = 0;
         return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, KTILES, 1, 1, st);
       });
     };
@@ -184,8 +233,7 @@ int s3od_linear_wgrad(int dtype, int Nout, int Kin, int rows, const void* dy, lo
     const int KTILES = cdiv(rows, KT<T>::BK);
     return with_cfg(1, [&](auto C) -> int {
       constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
-      int sp = split;
-      if (sp <= 0) { int tiles = cdiv(Nout, BM) * cdiv(Kin, BN); sp = max(1, min(KTILES / 8, 2048 / max(tiles, 1))); }
+      int sp = split > 0 ? split : wgrad_split<T, BM, BN, NST>(cdiv(Nout, BM) * cdiv(Kin, BN), KTILES);
       DenseMC<T, BM> la{(const T*)dy, lddy, rows, Nout};
       DenseMC<T, BN> lb{(const T*)x, ldx, rows, Kin};
       EpiWgrad e{dw, Nout, Kin, Kin, 1};
@@ -294,8 +342,7 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
     const int KTILES = cdiv(NPIX, KT<T>::BK);
     auto go = [&](auto bm, auto rl) -> int {
       constexpr int BM = decltype(bm)::value, BN = 128, NST = 2;
-      int sp = split;
-      if (sp <= 0) { int tiles = cdiv(M, BM) * cdiv(N, BN); sp = max(1, min(KTILES / 8, 2048 / max(tiles, 1))); }
+      int sp = split > 0 ? split : wgrad_split<T, BM, BN, NST>(cdiv(M, BM) * cdiv(N, BN), KTILES);
       DenseMC<T, BM> la{(const T*)dy, (long)Cout, NPIX, Cout};
       WgradB<T, BN, decltype(rl)::value> lb{}; lb.x = (const T*)x; lb.g = g; lb.NPIX = NPIX; lb.relu = relu_x;
       // taps > 1: the split-K atomics go to a workspace in the GEMM's own [Cout][tap][Cin] layout
@@ -331,7 +378,8 @@ int s3od_mask_heads_fwd(int dtype, int B, int H, int W, const void* feat, const 
     ConvFwdA<T, BM> la{}; la.x = (const T*)feat; la.g = g; la.M = M; la.relu = 0;
     DenseKC<T, BN> lb{(const T*)w1p, (long)K, N, K, 0};
     EpiHeads<T> e{logits, (T*)hsave, b1, w2, b2, M, H * W};
-    return launch_igemm<T, BM, BN>(la, lb, e, M, BN, cdiv(K, KT<T>::BK), 1, 1, st);
+    // 2 K stages: 67.6 KB of LDS -> 2 workgroups per CU, so one's epilogue overlaps the other's K loop
+    return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), 2>(la, lb, e, M, BN, cdiv(K, KT<T>::BK), 1, 1, st);
   });
   return 0;
 }

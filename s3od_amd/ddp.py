@@ -10,6 +10,8 @@ Works with gloo on CPU tensors too (tests).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -21,12 +23,15 @@ class GradSync:
         self.backend = dist.get_backend(group)
         self.works = []
         self.stream = None
+        # S3OD_DDP_REHEARSE=1: issue the collectives even at world size 1 (exercises the RCCL
+        # stream/event path on a one-GPU box; the mean over one rank is the identity)
+        self.rehearse = os.environ.get("S3OD_DDP_REHEARSE", "0") == "1"
         if model is not None:
             model.grad_ready_callback = self.on_ready
             model.grad_finish_callback = self.finish
 
     def on_ready(self, name, flat_slice):
-        if self.world == 1:
+        if self.world == 1 and not self.rehearse:
             return
         if flat_slice.is_cuda:
             if self.stream is None:

@@ -30,7 +30,9 @@ def lin(M, N, K, out_f32=False):
     f = lambda: lib()("s3od_linear_fwd", BF16, M, N, K, x, K, w, b, None, None, 0, None, N, None, 0, 0, o, N, int(out_f32),
                       None, N, 0, 0, 0, stream())
     t = timeit(f)
-    print(f"linear fwd M={M} N={N} K={K}: {t * 1e6:8.1f} us  {2 * M * N * K / t / 1e12:7.1f} TF/s")
+    tb = timeit(lambda: torch.matmul(x, w.t()))
+    print(f"linear fwd M={M} N={N} K={K}: {t * 1e6:8.1f} us  {2 * M * N * K / t / 1e12:7.1f} TF/s"
+          f"   (hipBLASLt torch.matmul yardstick {2 * M * N * K / tb / 1e12:7.1f} TF/s)")
 
 
 def dgrad(M, N, K):
@@ -86,7 +88,44 @@ def attn_bwd(B, N):
     print(f"attn bwd B={B} N={N}: {t * 1e6:8.1f} us  {10 * B * 12 * N * N * 64 / t / 1e12:7.1f} TF/s (5 GEMMs; 4 algorithmic)")
 
 
+def check():
+    """Numerics of linear fwd / dgrad / wgrad through the active tile config vs torch fp32."""
+    torch.manual_seed(0)
+    for (M, N, K) in ((2 * 4101 + 7, 2304, 768), (4101, 768, 3072), (300, 128, 64)):
+        x = torch.randn(M, K, device="cuda").bfloat16()
+        w = torch.randn(N, K, device="cuda").bfloat16()
+        b = torch.randn(N, device="cuda")
+        o = torch.empty(M, N, device="cuda", dtype=torch.float32)
+        lib()("s3od_linear_fwd", BF16, M, N, K, x, K, w, b, None, None, 0, None, N, None, 0, 0, o, N, 1,
+              None, N, 0, 0, 0, stream())
+        ref = x.float() @ w.float().t() + b
+        e1 = ((o - ref).norm() / ref.norm()).item()
+        dy = torch.randn(M, N, device="cuda").bfloat16()
+        dx = torch.empty(M, K, device="cuda", dtype=torch.float32)
+        lib()("s3od_linear_dgrad", BF16, M, K, N, dy, N, w, 0, None, K, dx, K, 1, 0, 0, 0, None, stream())
+        rd = dy.float() @ w.float()
+        e2 = ((dx - rd).norm() / rd.norm()).item()
+        dw = torch.zeros(N, K, device="cuda")
+        lib()("s3od_linear_wgrad", BF16, N, K, M, dy, N, x, K, dw, 0, stream())
+        rw = dy.float().t() @ x.float()
+        e3 = ((dw - rw).norm() / rw.norm()).item()
+        torch.cuda.synchronize()
+        ok = max(e1, e2, e3) < 1e-5
+        print(f"check M={M} N={N} K={K}: fwd {e1:.2e} dgrad {e2:.2e} wgrad {e3:.2e} {'OK' if ok else 'FAIL'}")
+        assert ok
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "check":
+        check()
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "ksweep":
+        for K in (64, 128, 256, 768, 1536, 3072):
+            lin(65536, 2304, K)
+        for K in (64, 768):
+            lin(65536, 256, K)
+            lin(4096, 2304, K)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "attn":
         attn(16, 4101)
         attn_bwd(16, 4101)
