@@ -5,7 +5,7 @@ CSRC := s3od_amd/csrc
 SRCS := $(wildcard $(CSRC)/*.hip)
 OBJS := $(patsubst $(CSRC)/%.hip,build/%.o,$(SRCS))
 HDRS := $(wildcard $(CSRC)/*.hpp)
-FLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result -munsafe-fp-atomics -mllvm -amdgpu-mfma-vgpr-form=1
+FLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -munsafe-fp-atomics -mllvm -amdgpu-mfma-vgpr-form=1
 
 all: s3od_amd/libs3od_hip.so
 

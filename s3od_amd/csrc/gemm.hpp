@@ -120,15 +120,15 @@ template <int RB> DEV int mc_logical_byte(int k, int phys) {
   return (((phys >> 5) ^ g) << 5) | (phys & 31);
 }
 
-template <typename T, int R> struct KCGeom {
-  static constexpr int NIW = R * 128 / 1024 / GEMM_WAVES, EPC = 16 / sizeof(T), BK = KT<T>::BK;
+template <typename T, int R, int NW = GEMM_WAVES> struct KCGeom {
+  static constexpr int NIW = R * 128 / 1024 / NW, EPC = 16 / sizeof(T), BK = KT<T>::BK;
   static_assert(NIW >= 1, "tile too small for the wave count");
   // row and logical element offset (within the k tile) of this lane's chunk of instruction i
   DEV static int row(int wave, int i, int lane) { return (wave * NIW + i) * 8 + (lane >> 3); }
   DEV static int kel(int wave, int i, int lane) { int r = row(wave, i, lane); return ((lane & 7) ^ ((r >> 1) & 7)) * EPC; }
 };
-template <typename T, int R> struct MCGeom {
-  static constexpr int NIW = R * 128 / 1024 / GEMM_WAVES, RB = R * sizeof(T), BK = KT<T>::BK;
+template <typename T, int R, int NW = GEMM_WAVES> struct MCGeom {
+  static constexpr int NIW = R * 128 / 1024 / NW, RB = R * sizeof(T), BK = KT<T>::BK;
   DEV static int krow(int wave, int i, int lane) { return ((wave * NIW + i) * 1024 + lane * 16) / RB; }
   DEV static int col(int wave, int i, int lane) {
     int o = ((wave * NIW + i) * 1024 + lane * 16) % RB;
@@ -136,9 +136,9 @@ template <typename T, int R> struct MCGeom {
   }
 };
 
-template <typename T, int R> struct DenseKC {          // X[row*ld + k]
+template <typename T, int R, int NW = GEMM_WAVES> struct DenseKC {          // X[row*ld + k]
   static constexpr bool KCL = true, RELU = false;
-  typedef KCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
+  typedef KCGeom<T, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* p; long ld; int nrows, K; int relu;
   unsigned vo[NIW]; int kel[NIW];
   HD unsigned long bytes() const { return ((unsigned long)(nrows - 1) * ld + K) * sizeof(T); }
@@ -166,9 +166,9 @@ template <typename T, int R> struct DenseKC {          // X[row*ld + k]
   }
 };
 
-template <typename T, int R> struct DenseMC {          // X[k*ld + col]
+template <typename T, int R, int NW = GEMM_WAVES> struct DenseMC {          // X[k*ld + col]
   static constexpr bool KCL = false, RELU = false;
-  typedef MCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
+  typedef MCGeom<T, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* p; long ld; int K, ncols;
   int relu = 0;
   unsigned vo[NIW]; int kr[NIW]; bool cv[NIW];
@@ -225,9 +225,9 @@ struct TapWalk {
 };
 
 // conv forward A operand: rows = output pixels (b,oy,ox) of RH x RW, k = tap*SC + c
-template <typename T, int R, bool RELU_ = false> struct ConvFwdA {
+template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct ConvFwdA {
   static constexpr bool KCL = true, RELU = RELU_;
-  typedef KCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
+  typedef KCGeom<T, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* x; ConvGeo g; int M; int relu;
   int iy0[NIW], ix0[NIW], pix0[NIW];      // top-left input pixel (may be outside) and its element offset + kel
   int kl[NIW];
@@ -286,9 +286,9 @@ template <typename T, int R, bool RELU_ = false> struct ConvFwdA {
 };
 
 // dgrad / ConvT A operand: rows = class pixels (b, y', x'), k = (jh*ntw + jw)*SC + c
-template <typename T, int R> struct ConvDgradA {
+template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradA {
   static constexpr bool KCL = true, RELU = false;
-  typedef KCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
+  typedef KCGeom<T, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* dy; ConvGeo g; int M;
   int relu = 0;
   int ry[NIW], rx[NIW], pix0[NIW], kl[NIW];
@@ -348,9 +348,9 @@ template <typename T, int R> struct ConvDgradA {
 };
 
 // dgrad / ConvT B operand (MC): B[k=(jh,jw,c)][n] = W[c][kh0+s*jh][kw0+s*jw][n], W repacked [C][KH][KW][N]
-template <typename T, int R> struct ConvDgradB {
+template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradB {
   static constexpr bool KCL = false, RELU = false;
-  typedef MCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
+  typedef MCGeom<T, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* w; ConvGeo g; int NC;     // NC = output channels of the dgrad (= conv input channels)
   int relu = 0;
   unsigned lo[NIW]; bool cv[NIW]; int kr[NIW];
@@ -399,9 +399,9 @@ template <typename T, int R> struct ConvDgradB {
 // wgrad B operand (MC gather): B[k=pix of the conv output grid RH x RW][n=(tap, cin)] = X[src][cin]
 // Fast path (RW % BK == 0): the 64 pixels of a K tile share one output row, so (b, oy, ox0) are
 // wave-uniform and interior tiles need no per-lane bounds test.
-template <typename T, int R, bool RELU_ = false> struct WgradB {
+template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct WgradB {
   static constexpr bool KCL = false, RELU = RELU_;
-  typedef MCGeom<T, R> G; static constexpr int NIW = G::NIW, BK = G::BK;
+  typedef MCGeom<T, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* x; ConvGeo g; int NPIX; int relu;   // g.SC = Cin of X, g.SH/SW = X dims, RH/RW = output grid
   int kh[NIW], kw[NIW], kr[NIW], cin[NIW]; unsigned lo[NIW]; bool cval[NIW];
   int nk, pb, poy, pox;                         // uniform walker (fast path)
@@ -680,165 +680,7 @@ __global__ void __launch_bounds__(GEMM_THREADS) igemm_kernel(LA la, LB lb, EPI e
       }
     }
     __syncthreads();
-    epi(ct, S::LDT, m0 + c0, n0, tid, S::CROWS, BN);
-  }
-}
-
-// ------------------------------------------------------------------ persistent variant
-// One workgroup per CU walks a list of output tiles (XCD-aware: the tiles of one XCD form a
-// contiguous row-major range, so its 32 CUs share A row panels and B in their L2).  The K-tile
-// stream runs ACROSS tiles: during the last K tile of tile i the loaders are re-pointed at tile
-// i+1 and its first K tile is DMA'd into the free stage, so that load and the epilogue of tile i
-// (C staged in 64-row chunks, stores left in flight) overlap instead of running back to back.
-// LDS: two K stages and a C-chunk region that aliases the stage just consumed:
-//   stage 0 = [0, STG), stage 1 = [STG+SLACK, 2*STG+SLACK); C region of stage 0 = [0, CB),
-//   of stage 1 = [STG, STG+CB)  (CB = STG+SLACK)  -> a C region never overlaps the other stage.
-// Wave grid 2 x 4 (per-wave 128 x 64): a 64-row C chunk is written by four waves.
-template <typename T, int BM, int BN> struct PShape {
-  typedef GemmShape<T, BM, BN, 2, 2> G;
-  static constexpr int CR = 64;
-  static constexpr int CB = CR * G::LDT * 4;
-  static constexpr int STG = G::STAGE;
-  static constexpr int SLACK = CB > STG ? CB - STG : 0;
-  static constexpr int LDS = 2 * STG + SLACK;
-  static_assert(LDS <= 160 * 1024, "LDS budget");
-  static_assert(BM % CR == 0 && G::TM % 16 == 0, "chunking");
-};
-
-template <typename T, int BM, int BN, class LA, class LB, class EPI>
-__global__ void __launch_bounds__(GEMM_THREADS) pgemm_kernel(LA la, LB lb, EPI epi, int KTILES, int split, int tiles_x, int tiles_y) {
-  typedef PShape<T, BM, BN> P;
-  typedef typename P::G S;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
-  const int wm = wave / S::WN, wn = wave % S::WN;
-  constexpr int MI = S::MI, NI = S::NI, KS = Mma<T>::KSTEPS;
-  const int ntiles = tiles_x * tiles_y * split;
-  // ---- this workgroup's tile list (WG b runs on XCD b & 7)
-  const int G = gridDim.x, b = blockIdx.x, x = b & 7, j = b >> 3;
-  const int ng = (G - x + 7) >> 3;                           // WGs on XCD x
-  int cum = 0;
-  for (int y = 0; y < x; y++) cum += (G - y + 7) >> 3;
-  const int lo = (int)((long)ntiles * cum / G), hi = (int)((long)ntiles * (cum + ng) / G);
-  int tile = lo + j;
-  if (tile >= hi) return;
-  const int per = (KTILES + split - 1) / split;
-  auto coords = [&](int tl, int& m0, int& n0, int& kt0, int& kt1) {
-    const int xy = tiles_x * tiles_y, z = tl / xy, r = tl - z * xy, by = r / tiles_x;
-    m0 = by * BM; n0 = (r - by * tiles_x) * BN;
-    kt0 = z * per; kt1 = min(KTILES, kt0 + per);
-  };
-  auto stage = [&](int st) -> char* { return smem + (st ? P::STG + P::SLACK : 0); };
-  auto cregion = [&](int st) -> float* { return (float*)(smem + (st ? P::STG : 0)); };
-
-  f32x4 acc[MI][NI];
-  typedef typename Mma<T>::frag frag;
-  frag fa[2][MI], fb[2][NI];
-  auto read_frags = [&](int buf, const char* stg, int kk) {
-    const char* As = stg;
-    const char* Bs = stg + S::ABYTES;
-#pragma unroll
-    for (int i = 0; i < MI; i++) fa[buf][i] = Frag<T, LA::KCL, BM>::read(As, wm * S::TM + i * 16, kk, lane);
-#pragma unroll
-    for (int q = 0; q < NI; q++) fb[buf][q] = Frag<T, LB::KCL, BN>::read(Bs, wn * S::TN + q * 16, kk, lane);
-  };
-  auto mfmas = [&](int buf) {
-    if constexpr (LA::RELU) {
-#pragma unroll
-      for (int i = 0; i < MI; i++) fa[buf][i] = relu_frag(fa[buf][i]);
-    }
-    if constexpr (LB::RELU) {
-#pragma unroll
-      for (int q = 0; q < NI; q++) fb[buf][q] = relu_frag(fb[buf][q]);
-    }
-#pragma unroll
-    for (int i = 0; i < MI; i++)
-#pragma unroll
-      for (int q = 0; q < NI; q++) acc[i][q] = Mma<T>::mma(fa[buf][i], fb[buf][q], acc[i][q]);
-  };
-
-  int m0, n0, kt0, kt1;
-  coords(tile, m0, n0, kt0, kt1);
-  la.setup(m0, tid);
-  lb.setup(n0, tid);
-  int cur = 0;
-  if (kt1 > kt0) { la.issue(kt0, stage(0)); lb.issue(kt0, stage(0) + S::ABYTES); }
-  while (true) {
-    const int nt = kt1 - kt0;
-    const int next = tile + ng;
-    const bool has_next = next < hi;
-    int nm0 = 0, nn0 = 0, nkt0 = 0, nkt1 = 0;
-    if (has_next) coords(next, nm0, nn0, nkt0, nkt1);
-#pragma unroll
-    for (int i = 0; i < MI; i++)
-#pragma unroll
-      for (int q = 0; q < NI; q++) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (nt > 0) {
-      wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();
-      read_frags(0, stage(cur), 0);
-    }
-    for (int t = 0; t < nt; ++t) {
-      const bool pre = t + 1 < nt;
-      char* nx = stage(cur ^ 1);
-      if (pre) {
-        la.issue(kt0 + t + 1, nx);
-        lb.issue(kt0 + t + 1, nx + S::ABYTES);
-      } else if (has_next && nkt1 > nkt0) {
-        // last K tile of this tile: re-point the loaders and start the next tile's first K tile
-        la.setup(nm0, tid);
-        lb.setup(nn0, tid);
-        la.issue(nkt0, nx);
-        lb.issue(nkt0, nx + S::ABYTES);
-      }
-      const char* stg = stage(cur);
-#pragma unroll
-      for (int kk = 0; kk < KS; kk++) {
-        const int bb = kk & 1;
-        if (kk + 1 < KS) {
-          read_frags(bb ^ 1, stg, kk + 1);
-        } else if (pre) {
-          wait_vmcnt<0>();
-          wait_lgkm0();
-          __builtin_amdgcn_s_barrier();
-          read_frags(bb ^ 1, nx, 0);
-        }
-        mfmas(bb);
-      }
-      if (pre) cur ^= 1;
-    }
-    if (nt == 0 && has_next && nkt1 > nkt0) {      // empty split-K range: still start the next tile
-      la.setup(nm0, tid);
-      lb.setup(nn0, tid);
-      la.issue(nkt0, stage(cur ^ 1));
-      lb.issue(nkt0, stage(cur ^ 1) + S::ABYTES);
-    }
-    // ---- epilogue of this tile: C chunks in the region of the stage just consumed.  Raw barriers
-    // (LDS waits only): __syncthreads() would also drain the next tile's K-tile DMA.
-    lds_barrier();
-    float* ct = cregion(cur);
-#pragma unroll
-    for (int c0 = 0; c0 < BM; c0 += P::CR) {
-      if (c0) lds_barrier();
-#pragma unroll
-      for (int i = 0; i < MI; i++) {
-        const int rb = wm * S::TM + i * 16;                  // wave-uniform
-        if (rb < c0 || rb >= c0 + P::CR) continue;
-#pragma unroll
-        for (int q = 0; q < NI; q++) {
-          int r = rb - c0 + (lane >> 4) * 4;
-          int c = wn * S::TN + q * 16 + (lane & 15);
-#pragma unroll
-          for (int e = 0; e < 4; e++) ct[(r + e) * S::LDT + c] = acc[i][q][e];
-        }
-      }
-      lds_barrier();
-      epi(ct, S::LDT, m0 + c0, n0, tid, P::CR, BN);
-    }
-    if (!has_next) break;
-    lds_barrier();                                           // C region free before it is re-filled
-    tile = next; m0 = nm0; n0 = nn0; kt0 = nkt0; kt1 = nkt1;
-    cur ^= 1;
+    epi(ct, S::LDT, m0 + c0, n0, tid, S::CROWS, BN, GEMM_THREADS);
   }
 }
 
@@ -846,10 +688,10 @@ __global__ void __launch_bounds__(GEMM_THREADS) pgemm_kernel(LA la, LB lb, EPI e
 // thread count is a multiple of the segments per row (every config but the N=96 head), a thread
 // keeps ONE column group and the loop has a compile-time trip count, so it unrolls and the LDS
 // reads / global stores of all rows are in flight together.
-template <class F> DEV void for_segments(const float* ct, int LDT, int BM, int BN, int m0, int n0, int M, int N, int tid, F f) {
+template <class F> DEV void for_segments(const float* ct, int LDT, int BM, int BN, int m0, int n0, int M, int N, int tid, int NT, F f) {
   const int spr = BN / 8;
-  if (GEMM_THREADS % spr == 0 && BM % (GEMM_THREADS / spr) == 0) {
-    const int rpi = GEMM_THREADS / spr, cs = tid % spr, r0 = tid / spr;
+  if (NT % spr == 0 && BM % (NT / spr) == 0) {
+    const int rpi = NT / spr, cs = tid % spr, r0 = tid / spr;
     const int n = n0 + cs * 8;
     if (n >= N) return;
 #pragma unroll
@@ -864,7 +706,7 @@ template <class F> DEV void for_segments(const float* ct, int LDT, int BM, int B
     return;
   }
   const int segs = BM * BN / 8;
-  for (int s = tid; s < segs; s += GEMM_THREADS) {
+  for (int s = tid; s < segs; s += NT) {
     int r = s / spr, cs = s - r * spr;
     int m = m0 + r, n = n0 + cs * 8;
     if (m < M && n < N) f(m, n, ct + r * LDT + cs * 8, r, cs * 8);
@@ -888,8 +730,8 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
   RowMap rm;
   float* csum = nullptr;                // optional: out[n] column sums (bias gradient), fp32 atomics
   DEV void prepare(int) {}
-  DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN) const {
-    // a thread always sees the same 8-column group (GEMM_THREADS % (BN/8) == 0), so its column
+  DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN, int NT) const {
+    // a thread always sees the same 8-column group (NT % (BN/8) == 0), so its column
     // partial sums live in registers until the block reduction below
     float cs8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     // per-column affine terms of this thread's (fixed) 8-column group, loaded once
@@ -904,8 +746,8 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
         h8[e] = (shift && ok) ? shift[nn + e] : 0.f;
       }
     }
-    const bool fixed_cols = GEMM_THREADS % (BN / 8) == 0;
-    for_segments(ct, LDT, BM, BN, m0, n0, M, N, tid, [&](int m, int n, const float* a, int, int) {
+    const bool fixed_cols = NT % (BN / 8) == 0;
+    for_segments(ct, LDT, BM, BN, m0, n0, M, N, tid, NT, [&](int m, int n, const float* a, int, int) {
       float pv[8], v[8], o[8];
       long orow = rm.map(m);
       if (fixed_cols) {
@@ -938,7 +780,7 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
     });
     if (stats) {
       // column statistics of pre over this tile's valid rows: 256 threads -> (col, row-phase)
-      int nph = GEMM_THREADS / BN;
+      int nph = NT / BN;
       int c = tid % BN, ph = tid / BN;
       int n = n0 + c;
       if (n < N) {
@@ -960,7 +802,7 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
 #pragma unroll
       for (int e = 0; e < 8; e++) red[tid * 8 + e] = cs8[e];
       __syncthreads();
-      const int spr = BN / 8, nph = GEMM_THREADS / spr;
+      const int spr = BN / 8, nph = NT / spr;
       if (tid < BN && n0 + tid < N) {
         const int g = tid >> 3, e = tid & 7;
         float s = 0.f;
@@ -976,9 +818,9 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
 struct EpiWgrad {
   float* dw; int M, N, Cx, taps;
   DEV void prepare(int) {}
-  DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN) const {
+  DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN, int NT) const {
     const int total = BM * BN;
-    for (int s = tid; s < total; s += GEMM_THREADS) {
+    for (int s = tid; s < total; s += NT) {
       int r = s / BN, c = s - r * BN;
       int m = m0 + r, n = n0 + c;
       if (m < M && n < N) {
@@ -989,24 +831,12 @@ struct EpiWgrad {
   }
 };
 
-// NST = 0 selects the persistent two-stage kernel (pgemm_kernel, one workgroup per CU).
 template <typename T, int BM, int BN, class LA, class LB, class EPI, int NST = 3>
 static int launch_igemm(LA la, LB lb, EPI epi, int M, int N, int KTILES, int split, int zdim_extra, hipStream_t st) {
   if (!la.buf_ok() || !lb.buf_ok()) {
     s3od_set_error("igemm: operand too large for a buffer descriptor or gather channels < %d", KT<T>::BK);
     return 22;
   }
-  if constexpr (NST == 0) {
-    typedef PShape<T, BM, BN> P;
-    auto kfn = pgemm_kernel<T, BM, BN, LA, LB, EPI>;
-    static bool attr = false;
-    if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, P::LDS); attr = true; }
-    const int tx = cdiv(N, BN), ty = cdiv(M, BM);
-    const long ntiles = (long)tx * ty * split * zdim_extra;
-    const int grid = (int)(ntiles < 256 ? ntiles : 256);
-    hipLaunchKernelGGL(kfn, dim3(grid), dim3(GEMM_THREADS), P::LDS, st, la, lb, epi, KTILES, split, tx, ty);
-    return s3od_check_launch("pgemm");
-  } else {
   typedef GemmShape<T, BM, BN, NST> S;
   auto kfn = igemm_kernel<T, BM, BN, NST, LA, LB, EPI>;
   static bool attr = false;
@@ -1014,5 +844,4 @@ static int launch_igemm(LA la, LB lb, EPI epi, int M, int N, int KTILES, int spl
   dim3 grid(cdiv(N, BN), cdiv(M, BM), split * zdim_extra);
   hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), S::LDS, st, la, lb, epi, KTILES, split);
   return s3od_check_launch("igemm");
-  }
 }

@@ -16,23 +16,22 @@ static RowMap dense_rm() { RowMap r{}; r.mode = 0; return r; }
 //   0: 256x128, 3 stages (1 WG/CU)   1: 128x128, 2 stages (2 WG/CU)   2: 128x128, 3 stages
 //   3: 256x128, 2 stages (BN is clamped to 64 for 64-channel convs: 256x64 x 2 stages = 80 KB)
 //   4: 256x256, 2 stages (1 WG/CU, per-wave 64x128; C staged in two 128-row halves)
-//   5: 256x256 persistent (pgemm_kernel: 1 WG/CU walks tiles, next tile's loads overlap the epilogue)
 #include <stdlib.h>
 static int gemm_cfg() {
   static int c = -2;
   if (c == -2) { const char* e = getenv("S3OD_GEMM_CFG"); c = e ? atoi(e) : -1; }
   return c;
 }
-template <int BM_, int BN_, int NST_> struct TileCfg { static constexpr int BM = BM_, BN = BN_, NST = NST_; };
+// W = waves that issue the operand loads (the loaders are built for that many waves)
+template <int BM_, int BN_, int NST_, int W_ = GEMM_WAVES> struct TileCfg { static constexpr int BM = BM_, BN = BN_, NST = NST_, W = W_; };
 // call f(TileCfg) for the selected config; `def` = per-op default config index
-template <class F> static int with_cfg(int def, F f) {
+template <typename T, class F> static int with_cfg(int def, F f) {
   int c = gemm_cfg(); if (c < 0) c = def;
   switch (c) {
     case 1: return f(TileCfg<128, 128, 2>{});
     case 2: return f(TileCfg<128, 128, 3>{});
     case 3: return f(TileCfg<256, 128, 2>{});
     case 4: return f(TileCfg<256, 256, 2>{});
-    case 5: return f(TileCfg<256, 256, 0>{});
     default: return f(TileCfg<256, 128, 3>{});
   }
 }
@@ -44,7 +43,7 @@ template <typename T> struct EpiQKV {
   T* q; T* k; T* v; const float* bias; const float* cs; const float* sn;
   int M, Ntok, P, H;
   DEV void prepare(int) {}
-  DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN) const {
+  DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN, int NT) const {
     // this thread's fixed 8-column group: bias of its columns and of their RoPE partners (d +- 32)
     float b8[8], bp8[8];
     {
@@ -52,8 +51,8 @@ template <typename T> struct EpiQKV {
 #pragma unroll
       for (int e = 0; e < 8; e++) { b8[e] = bias ? bias[nn + e] : 0.f; bp8[e] = bias ? bias[nn + dc + e] : 0.f; }
     }
-    const bool fixed_cols = GEMM_THREADS % (BN / 8) == 0;
-    for_segments(ct, LDT, BM, BN, m0, n0, M, 3 * H * 64, tid, [&](int m, int n, const float* a, int r, int c) {
+    const bool fixed_cols = NT % (BN / 8) == 0;
+    for_segments(ct, LDT, BM, BN, m0, n0, M, 3 * H * 64, tid, NT, [&](int m, int n, const float* a, int r, int c) {
       int which = n / (H * 64), nn = n - which * H * 64, h = nn >> 6, d0 = nn & 63;
       int b = m / Ntok, t = m - b * Ntok;
       float val[8];
@@ -94,11 +93,11 @@ template <typename T> struct EpiHeads {
   float* logits; T* hsave; const float* b1; const float* w2; const float* b2;
   int M, HW;
   DEV void prepare(int) {}
-  DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN) const {
+  DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN, int NT) const {
     // h = relu(acc + b1) is formed on the fly from the staged fp32 tile (no in-place pass)
     if (hsave) {
       const int segs = BM * 12;                               // 12 segments of 8 channels per row
-      for (int s = tid; s < segs; s += GEMM_THREADS) {
+      for (int s = tid; s < segs; s += NT) {
         int r = s / 12, c = (s - r * 12) * 8, m = m0 + r;
         if (m >= M) continue;
         const float4* src = (const float4*)(ct + r * LDT + c);
@@ -110,7 +109,7 @@ template <typename T> struct EpiHeads {
       }
     }
     // logit_k = b2[k] + sum_j relu(acc[32k + j] + b1[32k + j]) * w2[32k + j]; k is wave-uniform
-    for (int s = tid; s < 3 * BM; s += GEMM_THREADS) {
+    for (int s = tid; s < 3 * BM; s += NT) {
       int k = s / BM, r = s - k * BM;
       int m = m0 + r;
       if (m >= M) continue;
@@ -179,10 +178,10 @@ int s3od_linear_fwd(int dtype, int M, int N, int K, const void* x, long ldx, con
     const int KTILES = cdiv(K, KT<T>::BK);
     auto go = [&](auto tile, auto tout, auto tres) -> int {
       typedef decltype(tout) TO; typedef decltype(tres) TR;
-      return with_cfg(K >= 2048 ? 0 : 1, [&](auto C) -> int {
+      return with_cfg<T>(K >= 2048 ? 0 : 1, [&](auto C) -> int {
         constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
-        DenseKC<T, BM> la{(const T*)x, ldx, M, K, 0};
-        DenseKC<T, BN> lb{(const T*)w, (long)K, N, K, 0};
+        DenseKC<T, BM, decltype(C)::W> la{(const T*)x, ldx, M, K, 0};
+        DenseKC<T, BN, decltype(C)::W> lb{(const T*)w, (long)K, N, K, 0};
         EpiStd<TO, TR, T> e{(TO*)out, ldo, 0, bias, scale, shift, (const TR*)res1, ldr1, (const TR*)res2, ldr2,
                             (T*)pre, ldp, nullptr, act, M, N, rm};
         static const int epi_probe = dev_knob("S3OD_EPI_PROBE", 0);   // dev: 1 = skip the epilogue's stores
@@ -208,10 +207,10 @@ int s3od_linear_dgrad(int dtype, int M, int N, int K, const void* dy, long lddy,
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(K, KT<T>::BK);
-    return with_cfg(1, [&](auto C) -> int {
+    return with_cfg<T>(1, [&](auto C) -> int {
       constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
-      DenseKC<T, BM> la{(const T*)dy, lddy, M, K, 0};
-      DenseMC<T, BN> lb{(const T*)w, (long)N, K, N};
+      DenseKC<T, BM, decltype(C)::W> la{(const T*)dy, lddy, M, K, 0};
+      DenseMC<T, BN, decltype(C)::W> lb{(const T*)w, (long)N, K, N};
       if (out_f32) {
         // f32 output: aux is an f32 tensor to add (e.g. the residual-stream gradient, in place)
         EpiStd<float, float> e{(float*)dx, lddx, 0, nullptr, nullptr, nullptr, (const float*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, rm, colsum};
@@ -231,11 +230,11 @@ int s3od_linear_wgrad(int dtype, int Nout, int Kin, int rows, const void* dy, lo
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(rows, KT<T>::BK);
-    return with_cfg(1, [&](auto C) -> int {
+    return with_cfg<T>(4, [&](auto C) -> int {
       constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
       int sp = split > 0 ? split : wgrad_split<T, BM, BN, NST>(cdiv(Nout, BM) * cdiv(Kin, BN), KTILES);
-      DenseMC<T, BM> la{(const T*)dy, lddy, rows, Nout};
-      DenseMC<T, BN> lb{(const T*)x, ldx, rows, Kin};
+      DenseMC<T, BM, decltype(C)::W> la{(const T*)dy, lddy, rows, Nout};
+      DenseMC<T, BN, decltype(C)::W> lb{(const T*)x, ldx, rows, Kin};
       EpiWgrad e{dw, Nout, Kin, Kin, 1};
       return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, Nout, Kin, KTILES, sp, 1, st);
     });
@@ -249,10 +248,10 @@ int s3od_qkv_rope_fwd(int dtype, int B, int Ntok, int P, const void* x, const vo
   const int H = 12, D = 768, N = 3 * D, M = B * Ntok;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
-    return with_cfg(1, [&](auto C) -> int {
+    return with_cfg<T>(4, [&](auto C) -> int {
       constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
-      DenseKC<T, BM> la{(const T*)x, (long)D, M, D, 0};
-      DenseKC<T, BN> lb{(const T*)w, (long)D, N, D, 0};
+      DenseKC<T, BM, decltype(C)::W> la{(const T*)x, (long)D, M, D, 0};
+      DenseKC<T, BN, decltype(C)::W> lb{(const T*)w, (long)D, N, D, 0};
       EpiQKV<T> e{(T*)q, (T*)k, (T*)v, bias, cos_t, sin_t, M, Ntok, P, H};
       return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, cdiv(D, KT<T>::BK), 1, 1, st);
     });
@@ -275,11 +274,11 @@ int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int C
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(K, KT<T>::BK);
     auto go = [&](auto bn, auto rl) -> int {
-      return with_cfg(Cout <= 64 ? 3 : 1, [&](auto C) -> int {
+      return with_cfg<T>(Cout <= 64 ? 3 : 1, [&](auto C) -> int {
         constexpr int BM = decltype(C)::BM, NST = decltype(C)::NST;
         constexpr int BN = decltype(bn)::value < decltype(C)::BN ? decltype(bn)::value : decltype(C)::BN;
-        ConvFwdA<T, BM, decltype(rl)::value> la{}; la.x = (const T*)x; la.g = g; la.M = M; la.relu = relu_in;
-        DenseKC<T, BN> lb{(const T*)wp, (long)K, N, K, 0};
+        ConvFwdA<T, BM, decltype(rl)::value, decltype(C)::W> la{}; la.x = (const T*)x; la.g = g; la.M = M; la.relu = relu_in;
+        DenseKC<T, BN, decltype(C)::W> lb{(const T*)wp, (long)K, N, K, 0};
         EpiStd<T, T> e{(T*)out, (long)Cout, 0, bias, scale, shift, (const T*)res1, (long)Cout, (const T*)res2, (long)Cout,
                        (T*)pre, (long)Cout, stats, act, M, N, dense_rm(), colsum};
         return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, KTILES, 1, 1, st);
@@ -312,11 +311,11 @@ int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
         if (M == 0) continue;
         RowMap rm{}; rm.mode = 2; rm.RH = g.RH; rm.RW = g.RW; rm.OH = H; rm.OW = W; rm.s = stride; rm.py = py; rm.px = px;
         auto go = [&](auto bn) -> int {
-          return with_cfg(Cin <= 64 ? 3 : 1, [&](auto C) -> int {
+          return with_cfg<T>(Cin <= 64 ? 3 : 1, [&](auto C) -> int {
             constexpr int BM = decltype(C)::BM, NST = decltype(C)::NST;
             constexpr int BN = decltype(bn)::value < decltype(C)::BN ? decltype(bn)::value : decltype(C)::BN;
-            ConvDgradA<T, BM> la{}; la.dy = (const T*)dy; la.g = g; la.M = M;
-            ConvDgradB<T, BN> lb{}; lb.w = (const T*)wp; lb.g = g; lb.NC = Cin;
+            ConvDgradA<T, BM, decltype(C)::W> la{}; la.dy = (const T*)dy; la.g = g; la.M = M;
+            ConvDgradB<T, BN, decltype(C)::W> lb{}; lb.w = (const T*)wp; lb.g = g; lb.NC = Cin;
             EpiStd<T, T> e{(T*)dx, (long)Cin, 0, bias, scale, shift, (const T*)res1, (long)Cin, (const T*)res2, (long)Cin,
                            (T*)pre, (long)Cin, stats, act, M, N, rm, colsum};
             return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, cdiv(K, KT<T>::BK), 1, 1, st);

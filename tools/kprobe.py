@@ -11,6 +11,8 @@ which = sys.argv[1] if len(sys.argv) > 1 else "all"
 M = 16 * 4101
 if which in ("all", "attn"):
     attn(16, 4101)
+if which == "lin64":
+    lin(65536, 2304, 64)
 if which in ("all", "lin"):
     lin(M, 2304, 768)
 if which in ("all", "conv"):
