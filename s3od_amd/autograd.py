@@ -64,10 +64,12 @@ class _MaskLossFn(torch.autograd.Function):
         out = torch.empty(16 + B * M + B, dtype=torch.float32, device=dev)
         logits = logits.contiguous()
         masks = masks.contiguous().float()
-        lib()("s3od_mask_loss_fwd", logits, masks, pred_iou.contiguous().float(), B, M, HW, cfg["w_focal"], cfg["w_iou"],
-              cfg["w_bce"], cfg["w_mse"], cfg["lam"], 0.25, 2.0, sums, coef, iou_ws, diu, out, stream())
+        W = logits.shape[3]
+        w_ssim = cfg.get("w_ssim", 0.0)
+        lib()("s3od_mask_loss_fwd", logits, masks, pred_iou.contiguous().float(), B, M, HW, W, cfg["w_focal"], cfg["w_iou"],
+              cfg["w_bce"], w_ssim, cfg["w_mse"], cfg["lam"], 0.25, 2.0, sums, coef, iou_ws, diu, out, stream())
         fctx.save_for_backward(logits, masks, coef, iou_ws, diu)
-        fctx.dims = (B, M, HW)
+        fctx.dims = (B, M, HW, W, int(w_ssim != 0.0))
         fctx.mark_non_differentiable(out)
         return out[0], out
 
@@ -75,11 +77,11 @@ class _MaskLossFn(torch.autograd.Function):
     def backward(fctx, g_loss, g_out):
         from ._lib import lib, stream
         logits, masks, coef, iou_ws, diu = fctx.saved_tensors
-        B, M, HW = fctx.dims
+        B, M, HW, W, with_ssim = fctx.dims
         dl = torch.empty_like(logits)
         di = torch.empty((B, M), dtype=torch.float32, device=logits.device)
         g = g_loss.reshape(1).float().contiguous()
-        lib()("s3od_mask_loss_bwd", logits, masks, coef, iou_ws, diu, g, dl, di, B, M, HW, 0.25, 2.0, stream())
+        lib()("s3od_mask_loss_bwd", logits, masks, coef, iou_ws, diu, g, dl, di, B, M, HW, W, with_ssim, 0.25, 2.0, stream())
         return dl, di, None, None
 
 

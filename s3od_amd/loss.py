@@ -3,8 +3,8 @@
 Accepts the reference's Hydra criterion list (``config/loss/focal_iou.yaml`` /
 ``bce_iou_ssim.yaml``: dicts with name / weight / target_key / output_key / loss._target_) and
 runs the whole multi-mask loss — sigmoid, soft-IoU selection, argmax best mask, focal / BCE /
-IoU components with the decayed all-mask term and the aux MSE — as fused HIP kernels
-(``s3od_mask_loss_fwd/bwd``).  ``forward(outputs, targets, epoch) -> (loss, parts)`` with the
+IoU / SSIM components with the decayed all-mask term and the aux MSE — as fused HIP kernels
+(``s3od_mask_loss_fwd/bwd``; SSIM = separable 11x11 Gaussian filters over LDS tiles).  ``forward(outputs, targets, epoch) -> (loss, parts)`` with the
 same part names as the reference (each reduced by ``.mean()``).
 """
 from __future__ import annotations
@@ -46,9 +46,9 @@ class LossModule(nn.Module):
         self.decay_rate = float(decay_rate)
         self.mask_components = [c for c in self.components if c.target_key == "masks" and c.output_key == "pred_masks"]
         self.aux_components = [c for c in self.components if c not in self.mask_components]
-        w = {"focal": 0.0, "iou": 0.0, "bce": 0.0, "mse": 0.0}
+        w = {"focal": 0.0, "iou": 0.0, "bce": 0.0, "ssim": 0.0, "mse": 0.0}
         for c in self.mask_components:
-            if c.kind not in ("focal", "iou", "bce"):
+            if c.kind not in ("focal", "iou", "bce", "ssim"):
                 raise NotImplementedError(f"mask criterion {c.kind!r} is not fused on MI355X yet")
             w[c.kind] += c.weight
         for c in self.aux_components:
@@ -63,11 +63,12 @@ class LossModule(nn.Module):
         if pm.size(1) == 1:
             raise NotImplementedError("single-mask branch (loss.py:166-188) is the dinol variant; not built")
         lam = self.full_mask_lambda * math.exp(-self.decay_rate * epoch)
-        cfg = {"w_focal": self.w["focal"], "w_iou": self.w["iou"], "w_bce": self.w["bce"], "w_mse": self.w["mse"], "lam": lam}
+        cfg = {"w_focal": self.w["focal"], "w_iou": self.w["iou"], "w_bce": self.w["bce"], "w_ssim": self.w["ssim"],
+               "w_mse": self.w["mse"], "lam": lam}
         loss, packed = mask_loss(pm, outputs["pred_iou"], targets["masks"], cfg)
         B, M = pm.shape[:2]
         parts = {"best_iou": packed[1], "gt_ious": packed[2]}
-        for ci, kind in enumerate(("focal", "iou", "bce")):
+        for ci, kind in enumerate(("focal", "iou", "bce", "ssim")):
             if kind in self._names:
                 n = self._names[kind]
                 parts[f"{n}_best"] = packed[4 + 2 * ci]
@@ -84,6 +85,17 @@ FOCAL_IOU = [
      "loss": {"_target_": "synth_sod.model_training.loss.FocalLoss", "reduction": "none"}},
     {"name": "iou_loss", "target_key": "masks", "output_key": "pred_masks", "weight": 1.0,
      "loss": {"_target_": "synth_sod.model_training.loss.IoULoss", "smooth": 1e-6, "reduction": "none"}},
+    {"name": "mse_ious_loss", "target_key": "gt_ious", "output_key": "pred_iou", "weight": 0.05,
+     "loss": {"_target_": "torch.nn.MSELoss"}},
+]
+
+BCE_IOU_SSIM = [
+    {"name": "bce_loss", "target_key": "masks", "output_key": "pred_masks", "weight": 30,
+     "loss": {"_target_": "torch.nn.BCELoss", "reduction": "none"}},
+    {"name": "iou_loss", "target_key": "masks", "output_key": "pred_masks", "weight": 0.5,
+     "loss": {"_target_": "synth_sod.model_training.loss.IoULoss", "smooth": 1e-6, "reduction": "none"}},
+    {"name": "ssim_loss", "target_key": "masks", "output_key": "pred_masks", "weight": 10,
+     "loss": {"_target_": "synth_sod.model_training.loss.SSIMLoss", "reduction": "none"}},
     {"name": "mse_ious_loss", "target_key": "gt_ious", "output_key": "pred_iou", "weight": 0.05,
      "loss": {"_target_": "torch.nn.MSELoss"}},
 ]
