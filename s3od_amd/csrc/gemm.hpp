@@ -567,9 +567,9 @@ DEV void lds_barrier() { wait_lgkm0(); __builtin_amdgcn_s_barrier(); asm volatil
 // vmcnt is counted (the tile two steps ahead stays in flight across the barrier); there is
 // no __syncthreads() in the loop (it would drain vmcnt to 0: guide §5).
 // Block order is remapped so consecutive tiles of one row-panel share an XCD (guide T1).
-template <typename T, int BM, int BN, int NST, class LA, class LB, class EPI>
+template <typename T, int BM, int BN, int NST, class LA, class LB, class EPI, int WM_ = 0>
 __global__ void __launch_bounds__(GEMM_THREADS) igemm_kernel(LA la, LB lb, EPI epi, int KTILES, int split) {
-  typedef GemmShape<T, BM, BN, NST> S;
+  typedef GemmShape<T, BM, BN, NST, WM_> S;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int wm = wave / S::WN, wn = wave % S::WN;
@@ -831,14 +831,15 @@ struct EpiWgrad {
   }
 };
 
-template <typename T, int BM, int BN, class LA, class LB, class EPI, int NST = 3>
+// WM_: waves along M (0 = by tile shape); e.g. 512x64 tiles use WM_=8 for 64x64 per-wave tiles
+template <typename T, int BM, int BN, class LA, class LB, class EPI, int NST = 3, int WM_ = 0>
 static int launch_igemm(LA la, LB lb, EPI epi, int M, int N, int KTILES, int split, int zdim_extra, hipStream_t st) {
   if (!la.buf_ok() || !lb.buf_ok()) {
     s3od_set_error("igemm: operand too large for a buffer descriptor or gather channels < %d", KT<T>::BK);
     return 22;
   }
-  typedef GemmShape<T, BM, BN, NST> S;
-  auto kfn = igemm_kernel<T, BM, BN, NST, LA, LB, EPI>;
+  typedef GemmShape<T, BM, BN, NST, WM_> S;
+  auto kfn = igemm_kernel<T, BM, BN, NST, LA, LB, EPI, WM_>;
   static bool attr = false;
   if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS); attr = true; }
   dim3 grid(cdiv(N, BN), cdiv(M, BM), split * zdim_extra);

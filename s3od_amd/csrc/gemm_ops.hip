@@ -23,7 +23,9 @@ static int gemm_cfg() {
   return c;
 }
 // W = waves that issue the operand loads (the loaders are built for that many waves)
-template <int BM_, int BN_, int NST_, int W_ = GEMM_WAVES> struct TileCfg { static constexpr int BM = BM_, BN = BN_, NST = NST_, W = W_; };
+template <int BM_, int BN_, int NST_, int W_ = GEMM_WAVES, int WM_ = 0> struct TileCfg {
+  static constexpr int BM = BM_, BN = BN_, NST = NST_, W = W_, WM = WM_;
+};
 // call f(TileCfg) for the selected config; `def` = per-op default config index
 template <typename T, class F> static int with_cfg(int def, F f) {
   int c = gemm_cfg(); if (c < 0) c = def;
@@ -186,7 +188,7 @@ int s3od_linear_fwd(int dtype, int M, int N, int K, const void* x, long ldx, con
                             (T*)pre, ldp, nullptr, act, M, N, rm};
         static const int epi_probe = dev_knob("S3OD_EPI_PROBE", 0);   // dev: 1 = skip the epilogue's stores
         if (epi_probe == 1) e.M = 0;
-        return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, KTILES, 1, 1, st);
+        return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, M, N, KTILES, 1, 1, st);
       });
     };
     if (out_f32 && res_f32) return go(0, float{}, float{});
@@ -214,10 +216,10 @@ int s3od_linear_dgrad(int dtype, int M, int N, int K, const void* dy, long lddy,
       if (out_f32) {
         // f32 output: aux is an f32 tensor to add (e.g. the residual-stream gradient, in place)
         EpiStd<float, float> e{(float*)dx, lddx, 0, nullptr, nullptr, nullptr, (const float*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, rm, colsum};
-        return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, KTILES, 1, 1, st);
+        return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, M, N, KTILES, 1, 1, st);
       }
       EpiStd<T, T> e{(T*)dx, lddx, 0, nullptr, nullptr, nullptr, (const T*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, rm, colsum};
-      return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, KTILES, 1, 1, st);
+      return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, M, N, KTILES, 1, 1, st);
     });
   });
   return 0;
@@ -236,7 +238,7 @@ int s3od_linear_wgrad(int dtype, int Nout, int Kin, int rows, const void* dy, lo
       DenseMC<T, BM, decltype(C)::W> la{(const T*)dy, lddy, rows, Nout};
       DenseMC<T, BN, decltype(C)::W> lb{(const T*)x, ldx, rows, Kin};
       EpiWgrad e{dw, Nout, Kin, Kin, 1};
-      return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, Nout, Kin, KTILES, sp, 1, st);
+      return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, Nout, Kin, KTILES, sp, 1, st);
     });
   });
   return 0;
@@ -253,7 +255,7 @@ int s3od_qkv_rope_fwd(int dtype, int B, int Ntok, int P, const void* x, const vo
       DenseKC<T, BM, decltype(C)::W> la{(const T*)x, (long)D, M, D, 0};
       DenseKC<T, BN, decltype(C)::W> lb{(const T*)w, (long)D, N, D, 0};
       EpiQKV<T> e{(T*)q, (T*)k, (T*)v, bias, cos_t, sin_t, M, Ntok, P, H};
-      return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, cdiv(D, KT<T>::BK), 1, 1, st);
+      return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, M, N, cdiv(D, KT<T>::BK), 1, 1, st);
     });
   });
   return 0;
@@ -281,7 +283,7 @@ int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int C
         DenseKC<T, BN, decltype(C)::W> lb{(const T*)wp, (long)K, N, K, 0};
         EpiStd<T, T> e{(T*)out, (long)Cout, 0, bias, scale, shift, (const T*)res1, (long)Cout, (const T*)res2, (long)Cout,
                        (T*)pre, (long)Cout, stats, act, M, N, dense_rm(), colsum};
-        return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, KTILES, 1, 1, st);
+        return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, M, N, KTILES, 1, 1, st);
       });
     };
     if (relu_in) {
@@ -318,7 +320,7 @@ int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
             ConvDgradB<T, BN, decltype(C)::W> lb{}; lb.w = (const T*)wp; lb.g = g; lb.NC = Cin;
             EpiStd<T, T> e{(T*)dx, (long)Cin, 0, bias, scale, shift, (const T*)res1, (long)Cin, (const T*)res2, (long)Cin,
                            (T*)pre, (long)Cin, stats, act, M, N, rm, colsum};
-            return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, cdiv(K, KT<T>::BK), 1, 1, st);
+            return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, M, N, cdiv(K, KT<T>::BK), 1, 1, st);
           });
         };
         int rc = Cin <= 64 ? go(std::integral_constant<int, 64>{}) : go(std::integral_constant<int, 128>{});

@@ -5,12 +5,13 @@ from pathlib import Path
 import torch
 
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
-from tools.gemm_bench import lin, attn, dgrad, wgrad, conv  # noqa: E402
+from tools.gemm_bench import lin, attn, attn_bwd, dgrad, wgrad, conv  # noqa: E402
 
 which = sys.argv[1] if len(sys.argv) > 1 else "all"
 M = 16 * 4101
 if which in ("all", "attn"):
     attn(16, 4101)
+    attn_bwd(16, 4101)
 if which == "lin64":
     lin(65536, 2304, 64)
 if which in ("all", "lin"):
