@@ -22,7 +22,8 @@ class FusedAdamW(torch.optim.Optimizer):
         self._tab_key = None
 
     def _table(self, items, dev):
-        key = tuple((p.data_ptr(), p.grad.data_ptr() if p.grad is not None else 0) for p, _ in items)
+        key = tuple((p.data_ptr(), p.grad.data_ptr() if p.grad is not None else 0,
+                     self.state[p]["exp_avg"].data_ptr(), self.state[p]["exp_avg_sq"].data_ptr()) for p, _ in items)
         lrs = torch.tensor([g["lr"] for _, g in items], dtype=torch.float32)
         if key != self._tab_key:
             ptrs, sizes, ct, co = [], [], [], []
@@ -42,6 +43,11 @@ class FusedAdamW(torch.optim.Optimizer):
         self._tab["lrs"] = lrs.to(dev, non_blocking=True)
         return self._tab
 
+    def load_state_dict(self, state_dict):
+        """torch.optim.AdamW-compatible state (the device pointer table is rebuilt)."""
+        super().load_state_dict(state_dict)
+        self._tab, self._tab_key = None, None
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -56,14 +62,17 @@ class FusedAdamW(torch.optim.Optimizer):
                     continue
                 st = self.state[p]
                 if not st:
-                    st["step"] = 0
+                    # torch.optim.AdamW layout (step as a float tensor) so state_dicts interchange
+                    st["step"] = torch.tensor(0.0)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                if not torch.is_tensor(st["step"]):
+                    st["step"] = torch.tensor(float(st["step"]))
                 st["step"] += 1
                 items.append((p, g))
         if not items:
             return loss
-        steps = {self.state[p]["step"] for p, _ in items}
+        steps = {int(self.state[p]["step"].item()) for p, _ in items}
         hyper = {(g["betas"], g["eps"], g["weight_decay"]) for _, g in items}
         if len(steps) != 1 or len(hyper) != 1:
             raise NotImplementedError("FusedAdamW: all stepped parameters must share step count and betas/eps/wd")
