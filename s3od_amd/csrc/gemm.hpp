@@ -112,6 +112,21 @@ DEV void blds16(__amdgpu_buffer_rsrc_t r, unsigned voff, char* lds_wave_base) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_wave_base, 16, voff, 0, 0, 0);
 }
 DEV int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// Where a loader's 16-B-per-lane chunk i goes.  Every loader computes one buffer offset per chunk
+// (source-side swizzle, OOB -> zeros) and hands it to a sink:
+//   DmaSink  LDS-DMA straight into the lane-linear LDS image (buffer_load_dwordx4 ... lds)
+//   RegSink  buffer_load_dwordx4 into registers; commit() later writes them to the same LDS
+//            positions with ds_write_b128 (register staging: no LDS-DMA issue cost per KiB)
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+struct DmaSink {
+  char* base;                                    // tile + wave * NIW * 1024
+  DEV void operator()(int i, __amdgpu_buffer_rsrc_t r, unsigned voff) const { blds16(r, voff, base + i * 1024); }
+};
+struct RegSink {
+  u32x4_t* regs;
+  DEV void operator()(int i, __amdgpu_buffer_rsrc_t r, unsigned voff) const { regs[i] = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0); }
+};
 #define HD __host__ __device__
 
 template <int RB> DEV int mc_logical_byte(int k, int phys) {
@@ -152,17 +167,24 @@ template <typename T, int R, int NW = GEMM_WAVES> struct DenseKC {          // X
       vo[i] = r < nrows ? (unsigned)(((long)r * ld + kel[i]) * sizeof(T)) : BUF_OOB;
     }
   }
-  DEV void issue(int kt, char* tile) {
-    const int wave = wave_id();
+  DEV void issue(int kt, char* tile) { issue_to(kt, DmaSink{tile + wave_id() * NIW * 1024}); }
+  // register staging: chunk i of this lane -> regs[i]; commit(tile, regs) stores it to LDS
+  DEV void issue_regs(int kt, u32x4_t* regs) { issue_to(kt, RegSink{regs}); }
+  DEV void commit(char* tile, const u32x4_t* regs) const {
+    char* b = tile + wave_id() * NIW * 1024 + (threadIdx.x & 63) * 16;
+#pragma unroll
+    for (int i = 0; i < NIW; i++) *(u32x4_t*)(b + i * 1024) = regs[i];
+  }
+  template <class SK> DEV void issue_to(int kt, SK sk) {
     const auto rs = make_rsrc(p, bytes());
     const unsigned adv = (unsigned)(kt * BK * sizeof(T));
     if ((kt + 1) * BK > K) {          // K tail (uniform branch)
 #pragma unroll
-      for (int i = 0; i < NIW; i++) blds16(rs, kt * BK + kel[i] < K ? vo[i] + adv : BUF_OOB, tile + (wave * NIW + i) * 1024);
+      for (int i = 0; i < NIW; i++) sk(i, rs, kt * BK + kel[i] < K ? vo[i] + adv : BUF_OOB);
       return;
     }
 #pragma unroll
-    for (int i = 0; i < NIW; i++) blds16(rs, vo[i] + adv, tile + (wave * NIW + i) * 1024);
+    for (int i = 0; i < NIW; i++) sk(i, rs, vo[i] + adv);
   }
 };
 
@@ -184,17 +206,24 @@ template <typename T, int R, int NW = GEMM_WAVES> struct DenseMC {          // X
       vo[i] = (unsigned)(((long)kr[i] * ld + cl) * sizeof(T));
     }
   }
-  DEV void issue(int kt, char* tile) {
-    const int wave = wave_id();
+  DEV void issue(int kt, char* tile) { issue_to(kt, DmaSink{tile + wave_id() * NIW * 1024}); }
+  // register staging: chunk i of this lane -> regs[i]; commit(tile, regs) stores it to LDS
+  DEV void issue_regs(int kt, u32x4_t* regs) { issue_to(kt, RegSink{regs}); }
+  DEV void commit(char* tile, const u32x4_t* regs) const {
+    char* b = tile + wave_id() * NIW * 1024 + (threadIdx.x & 63) * 16;
+#pragma unroll
+    for (int i = 0; i < NIW; i++) *(u32x4_t*)(b + i * 1024) = regs[i];
+  }
+  template <class SK> DEV void issue_to(int kt, SK sk) {
     const auto rs = make_rsrc(p, bytes());
     const unsigned adv = (unsigned)((long)kt * BK * ld * sizeof(T));
     if ((kt + 1) * BK > K) {          // K tail (uniform branch)
 #pragma unroll
-      for (int i = 0; i < NIW; i++) blds16(rs, cv[i] && kt * BK + kr[i] < K ? vo[i] + adv : BUF_OOB, tile + (wave * NIW + i) * 1024);
+      for (int i = 0; i < NIW; i++) sk(i, rs, cv[i] && kt * BK + kr[i] < K ? vo[i] + adv : BUF_OOB);
       return;
     }
 #pragma unroll
-    for (int i = 0; i < NIW; i++) blds16(rs, cv[i] ? vo[i] + adv : BUF_OOB, tile + (wave * NIW + i) * 1024);
+    for (int i = 0; i < NIW; i++) sk(i, rs, cv[i] ? vo[i] + adv : BUF_OOB);
   }
 };
 
@@ -251,8 +280,15 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Con
     }
     tw = TapWalk{};
   }
-  DEV void issue(int kt, char* tile) {
-    const int wave = wave_id();
+  DEV void issue(int kt, char* tile) { issue_to(kt, DmaSink{tile + wave_id() * NIW * 1024}); }
+  // register staging: chunk i of this lane -> regs[i]; commit(tile, regs) stores it to LDS
+  DEV void issue_regs(int kt, u32x4_t* regs) { issue_to(kt, RegSink{regs}); }
+  DEV void commit(char* tile, const u32x4_t* regs) const {
+    char* b = tile + wave_id() * NIW * 1024 + (threadIdx.x & 63) * 16;
+#pragma unroll
+    for (int i = 0; i < NIW; i++) *(u32x4_t*)(b + i * 1024) = regs[i];
+  }
+  template <class SK> DEV void issue_to(int kt, SK sk) {
     const auto rs = make_rsrc(x, bytes());
     if (g.SC % BK) {                 // channels not a multiple of BK: per-lane tap (rare shapes)
       tw.step_any(kt, BK, g.SC, g.KW);
@@ -265,7 +301,7 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Con
         int iy = iy0[i] + th, ix = ix0[i] + tww;
         bool ok = tw.tap + (int)wr < g.KH * g.KW && (unsigned)iy < (unsigned)g.SH && (unsigned)ix < (unsigned)g.SW;
         int off = pix0[i] - kl[i] + (th * g.SW + tww) * g.SC + (wr ? c - g.SC : c);
-        blds16(rs, ok ? (unsigned)off * (unsigned)sizeof(T) : BUF_OOB, tile + (wave * NIW + i) * 1024);
+        sk(i, rs, ok ? (unsigned)off * (unsigned)sizeof(T) : BUF_OOB);
       }
       return;
     }
@@ -281,7 +317,7 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Con
     }
     const unsigned cb = (unsigned)(tw.c0 * sizeof(T));
 #pragma unroll
-    for (int i = 0; i < NIW; i++) blds16(rs, base[i] + cb, tile + (wave * NIW + i) * 1024);
+    for (int i = 0; i < NIW; i++) sk(i, rs, base[i] + cb);
   }
 };
 
@@ -312,8 +348,15 @@ template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradA {
     }
     tw = TapWalk{};
   }
-  DEV void issue(int kt, char* tile) {
-    const int wave = wave_id();
+  DEV void issue(int kt, char* tile) { issue_to(kt, DmaSink{tile + wave_id() * NIW * 1024}); }
+  // register staging: chunk i of this lane -> regs[i]; commit(tile, regs) stores it to LDS
+  DEV void issue_regs(int kt, u32x4_t* regs) { issue_to(kt, RegSink{regs}); }
+  DEV void commit(char* tile, const u32x4_t* regs) const {
+    char* b = tile + wave_id() * NIW * 1024 + (threadIdx.x & 63) * 16;
+#pragma unroll
+    for (int i = 0; i < NIW; i++) *(u32x4_t*)(b + i * 1024) = regs[i];
+  }
+  template <class SK> DEV void issue_to(int kt, SK sk) {
     const auto rs = make_rsrc(dy, bytes());
     const int TW = g.ntw > 0 ? g.ntw : 1;
     if (g.SC % BK) {                 // channels not a multiple of BK: per-lane tap (rare shapes)
@@ -327,7 +370,7 @@ template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradA {
         int sy = ry[i] - th, sx = rx[i] - tww;
         bool ok = tw.tap + (int)wr < g.nth * g.ntw && (unsigned)sy < (unsigned)g.SH && (unsigned)sx < (unsigned)g.SW;
         int off = pix0[i] - kl[i] - (th * g.SW + tww) * g.SC + (wr ? c - g.SC : c);
-        blds16(rs, ok ? (unsigned)off * (unsigned)sizeof(T) : BUF_OOB, tile + (wave * NIW + i) * 1024);
+        sk(i, rs, ok ? (unsigned)off * (unsigned)sizeof(T) : BUF_OOB);
       }
       return;
     }
@@ -343,7 +386,7 @@ template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradA {
     }
     const unsigned cb = (unsigned)(tw.c0 * sizeof(T));
 #pragma unroll
-    for (int i = 0; i < NIW; i++) blds16(rs, base[i] + cb, tile + (wave * NIW + i) * 1024);
+    for (int i = 0; i < NIW; i++) sk(i, rs, base[i] + cb);
   }
 };
 
@@ -367,8 +410,15 @@ template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradB {
     }
     tw = TapWalk{};
   }
-  DEV void issue(int kt, char* tile) {
-    const int wave = wave_id();
+  DEV void issue(int kt, char* tile) { issue_to(kt, DmaSink{tile + wave_id() * NIW * 1024}); }
+  // register staging: chunk i of this lane -> regs[i]; commit(tile, regs) stores it to LDS
+  DEV void issue_regs(int kt, u32x4_t* regs) { issue_to(kt, RegSink{regs}); }
+  DEV void commit(char* tile, const u32x4_t* regs) const {
+    char* b = tile + wave_id() * NIW * 1024 + (threadIdx.x & 63) * 16;
+#pragma unroll
+    for (int i = 0; i < NIW; i++) *(u32x4_t*)(b + i * 1024) = regs[i];
+  }
+  template <class SK> DEV void issue_to(int kt, SK sk) {
     const auto rs = make_rsrc(w, bytes());
     const int TW = g.ntw > 0 ? g.ntw : 1;
     if (g.SC % BK) {                 // a tile spans taps tap / tap+1 (rows c0+kr >= SC wrap)
@@ -383,7 +433,7 @@ template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradB {
       for (int i = 0; i < NIW; i++) {
         bool wr = tw.c0 + kr[i] >= g.SC;
         bool ok = cv[i] && (wr ? tv1 : tv0);
-        blds16(rs, ok ? lo[i] + (wr ? u1 : u0) : BUF_OOB, tile + (wave * NIW + i) * 1024);
+        sk(i, rs, ok ? lo[i] + (wr ? u1 : u0) : BUF_OOB);
       }
       return;
     }
@@ -392,7 +442,7 @@ template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradB {
     const int kh = g.kh0 + g.s * tw.th, kw = g.kw0 + g.s * tw.tw;
     const unsigned uo = (unsigned)((((long)tw.c0 * g.KH + kh) * g.KW + kw) * NC * sizeof(T));
 #pragma unroll
-    for (int i = 0; i < NIW; i++) blds16(rs, (tv && cv[i]) ? lo[i] + uo : BUF_OOB, tile + (wave * NIW + i) * 1024);
+    for (int i = 0; i < NIW; i++) sk(i, rs, (tv && cv[i]) ? lo[i] + uo : BUF_OOB);
   }
 };
 
@@ -421,8 +471,15 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Wgr
     }
     nk = -1;
   }
-  DEV void issue(int kt, char* tile) {
-    const int wave = wave_id();
+  DEV void issue(int kt, char* tile) { issue_to(kt, DmaSink{tile + wave_id() * NIW * 1024}); }
+  // register staging: chunk i of this lane -> regs[i]; commit(tile, regs) stores it to LDS
+  DEV void issue_regs(int kt, u32x4_t* regs) { issue_to(kt, RegSink{regs}); }
+  DEV void commit(char* tile, const u32x4_t* regs) const {
+    char* b = tile + wave_id() * NIW * 1024 + (threadIdx.x & 63) * 16;
+#pragma unroll
+    for (int i = 0; i < NIW; i++) *(u32x4_t*)(b + i * 1024) = regs[i];
+  }
+  template <class SK> DEV void issue_to(int kt, SK sk) {
     const auto rs = make_rsrc(x, bytes());
     if (g.RW % BK == 0) {
       if (kt != nk) { int k = kt * BK; int hw = g.RH * g.RW; pb = k / hw; int r = k - pb * hw; poy = r / g.RW; pox = r - poy * g.RW; }
@@ -434,13 +491,13 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Wgr
       const bool interior = iy0 >= 0 && iy0 + g.KH <= g.SH && ix0 >= 0 && ix0 + (BK - 1) * g.s + g.KW <= g.SW;
       if (live && interior) {
 #pragma unroll
-        for (int i = 0; i < NIW; i++) blds16(rs, cval[i] ? lo[i] + uo : BUF_OOB, tile + (wave * NIW + i) * 1024);
+        for (int i = 0; i < NIW; i++) sk(i, rs, cval[i] ? lo[i] + uo : BUF_OOB);
       } else {
 #pragma unroll
         for (int i = 0; i < NIW; i++) {
           int iy = iy0 + kh[i], ix = ix0 + kr[i] * g.s + kw[i];
           bool ok = live && cval[i] && (unsigned)iy < (unsigned)g.SH && (unsigned)ix < (unsigned)g.SW;
-          blds16(rs, ok ? lo[i] + uo : BUF_OOB, tile + (wave * NIW + i) * 1024);
+          sk(i, rs, ok ? lo[i] + uo : BUF_OOB);
         }
       }
       return;
@@ -461,7 +518,7 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Wgr
       int iy = qy[i] * g.s - g.p + kh[i], ix = qx[i] * g.s - g.p + kw[i];
       bool ok = cval[i] && qb[i] < g.B && (unsigned)iy < (unsigned)g.SH && (unsigned)ix < (unsigned)g.SW;
       unsigned v = (unsigned)(((((long)qb[i] * g.SH + iy) * g.SW + ix) * g.SC + cin[i]) * (long)sizeof(T));
-      blds16(rs, ok ? v : BUF_OOB, tile + (wave * NIW + i) * 1024);
+      sk(i, rs, ok ? v : BUF_OOB);
       qx[i] += BK;
       while (qx[i] >= g.RW) { qx[i] -= g.RW; if (++qy[i] >= g.RH) { qy[i] = 0; qb[i]++; } }
     }
@@ -838,11 +895,13 @@ static int launch_igemm(LA la, LB lb, EPI epi, int M, int N, int KTILES, int spl
     s3od_set_error("igemm: operand too large for a buffer descriptor or gather channels < %d", KT<T>::BK);
     return 22;
   }
-  typedef GemmShape<T, BM, BN, NST, WM_> S;
-  auto kfn = igemm_kernel<T, BM, BN, NST, LA, LB, EPI, WM_>;
-  static bool attr = false;
-  if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS); attr = true; }
-  dim3 grid(cdiv(N, BN), cdiv(M, BM), split * zdim_extra);
-  hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), S::LDS, st, la, lb, epi, KTILES, split);
-  return s3od_check_launch("igemm");
+  {
+    typedef GemmShape<T, BM, BN, NST, WM_> S;
+    auto kfn = igemm_kernel<T, BM, BN, NST, LA, LB, EPI, WM_>;
+    static bool attr = false;
+    if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS); attr = true; }
+    dim3 grid(cdiv(N, BN), cdiv(M, BM), split * zdim_extra);
+    hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), S::LDS, st, la, lb, epi, KTILES, split);
+    return s3od_check_launch("igemm");
+  }
 }
