@@ -675,8 +675,10 @@ __global__ void __launch_bounds__(GEMM_THREADS) igemm_kernel(LA la, LB lb, EPI e
 #pragma unroll
     for (int i = 0; i < MI; i++)
 #pragma unroll
-      for (int j = 0; j < NI; j++) acc[i][j] = Mma<T>::mma(fa[buf][i], fb[buf][j], acc[i][j]);
+      for (int j = 0; j < NI; j++) acc[i][j] = Mma<T>::mma(fb[buf][j], fa[buf][i], acc[i][j]);
   };
+  // (B, A operand order: acc[i][j] holds the 16x16 block TRANSPOSED, so lane (g, l) owns
+  //  C[m = i*16 + l][n = j*16 + 4g .. 4g+3] -- four consecutive columns -> one 16-B LDS store)
 
   const int nt = kt1 - kt0;
   constexpr int PD = NST - 1;                 // LDS-DMA prefetch distance (tiles in flight)
@@ -730,10 +732,9 @@ __global__ void __launch_bounds__(GEMM_THREADS) igemm_kernel(LA la, LB lb, EPI e
       if (rb < c0 || rb >= c0 + S::CROWS) continue;
 #pragma unroll
       for (int j = 0; j < NI; j++) {
-        int r = rb - c0 + (lane >> 4) * 4;
-        int c = wn * S::TN + j * 16 + (lane & 15);
-#pragma unroll
-        for (int e = 0; e < 4; e++) ct[(r + e) * S::LDT + c] = acc[i][j][e];
+        int r = rb - c0 + (lane & 15);
+        int c = wn * S::TN + j * 16 + (lane >> 4) * 4;
+        *(float4*)(ct + r * S::LDT + c) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
       }
     }
     __syncthreads();
