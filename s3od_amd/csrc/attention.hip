@@ -285,8 +285,13 @@ namespace {
 // 64-row x 64-d tile image used for both row reads (ds_read_b128 / scalar) and transposed reads
 template <typename T> struct Img;
 template <> struct Img<bf16> {
+  // 16-B slot XOR f((row >> 1) & 7) with f = (0,2,4,6,5,7,1,3): conflict-free for BOTH the
+  // row-fragment ds_read_b128 and the transposed ds_read_b64_tr_b16 patterns (exhaustive search
+  // over the 8! slot permutations against the gfx950 lane groups; the plain (row>>1)&7 XOR left
+  // the transposed reads 2-way conflicted)
   static constexpr int BYTES = 64 * 128;
-  DEV static int at(int row, int byte) { return row * 128 + ((((byte >> 4) ^ ((row >> 1) & 7)) << 4) | (byte & 15)); }
+  DEV static int swz(int row) { return (0x31756420u >> (((row >> 1) & 7) * 4)) & 7; }
+  DEV static int at(int row, int byte) { return row * 128 + ((((byte >> 4) ^ swz(row)) << 4) | (byte & 15)); }
 };
 template <> struct Img<float> {
   static constexpr int BYTES = 64 * 272;
