@@ -64,3 +64,24 @@ def test_forward_bf16(model, name):
     assert agree > 0.98
     assert rel_l2(out["pred_iou"].cpu().numpy(), g["pred_iou"]) < 3e-2
     model.compute_dtype = "f32"
+
+
+@pytest.mark.parametrize("shape", [(1, 3, 384, 512), (2, 3, 272, 208)])
+def test_forward_strict_vs_oracle_ragged(model, shape):
+    """Shapes the goldens do not cover (non-square, patch grids 24x32 and 17x13 -> GEMM / attention
+    tails in every kernel), against the oracle (pinned to the reference by tests/test_oracle_golden.py)
+    on the same synthetic weights: strict f32, max-rel <= 2e-4, argmax IoU index bit-exact."""
+    from oracle import s3od_oracle as O
+    from s3od_amd.weights import synthetic_state_dict
+    sd = {k: torch.from_numpy(v) for k, v in synthetic_state_dict(0).items()}
+    torch.manual_seed(1)
+    x = torch.randn(*shape)
+    with torch.no_grad():
+        ref = O.forward(x, sd)
+    model.compute_dtype = "f32"
+    with torch.no_grad():
+        out = model(x.cuda())
+    torch.cuda.synchronize()
+    assert rel_max(out["pred_masks"].cpu().numpy(), ref["pred_masks"].numpy()) < 2e-4
+    assert rel_max(out["pred_iou"].cpu().numpy(), ref["pred_iou"].numpy()) < 2e-4
+    assert (out["pred_iou"].cpu().numpy().argmax(1) == ref["pred_iou"].numpy().argmax(1)).all()
