@@ -270,15 +270,30 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const T* __restrict__ Q, 
 
 // ===================================================================================== backward
 // delta[bh][q] = sum_d dO[b][q][h*64+d] * O[b][q][h*64+d]
+// one thread per 8 consecutive d of one (token, head): 16-B loads over the contiguous token rows,
+// the 8 partial dots of a head reduced with 3 lane shuffles (consecutive lanes)
 template <typename T>
 __global__ void attn_delta_kernel(const T* __restrict__ O, const T* __restrict__ dO, float* __restrict__ delta, int N, int H, int BH) {
-  int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;   // row = bh*N + q
-  if (row >= BH * N) return;
-  int bh = row / N, q = row - bh * N, b = bh / H, h = bh - b * H;
-  long off = ((long)b * N + q) * (H * 64) + h * 64 + lane;
-  float v = to_f<T>(O[off]) * to_f<T>(dO[off]);
-  v = warp_sum(v);
-  if (lane == 0) delta[row] = v;
+  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;          // chunk over [B*N][H][8]
+  const long total = (long)BH * N * 8;
+  float v = 0.f;
+  const bool live = c < total;
+  long tok = 0; int h = 0;
+  if (live) {
+    tok = c / (H * 8);
+    const int rem = (int)(c - tok * (H * 8));
+    h = rem >> 3;
+    float a[8], d[8];
+    load8<T>(O + c * 8, a);
+    load8<T>(dO + c * 8, d);
+#pragma unroll
+    for (int e = 0; e < 8; e++) v += a[e] * d[e];
+  }
+  v += __shfl_xor(v, 1); v += __shfl_xor(v, 2); v += __shfl_xor(v, 4);
+  if (live && (c & 7) == 0) {
+    const long b = tok / N, q = tok - b * N;
+    delta[(b * H + h) * N + q] = v;
+  }
 }
 
 namespace {
@@ -654,7 +669,7 @@ int s3od_attn_bwd(int dtype, const void* q, const void* k, const void* v, const 
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(cdiv(N, 128), B * H);
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(attn_delta_kernel<T>, dim3(cdiv((long)B * H * N, 4)), dim3(256), 0, st, (const T*)o, (const T*)dout, delta, N, H, B * H);
+    hipLaunchKernelGGL(attn_delta_kernel<T>, dim3(cdiv((long)B * H * N * 8, 256)), dim3(256), 0, st, (const T*)o, (const T*)dout, delta, N, H, B * H);
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<T>, grid, dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse, delta,
                        (T*)dk, (T*)dv, N, H);
     hipLaunchKernelGGL(attn_bwd_dq_kernel<T>, grid, dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse, delta,
