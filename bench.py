@@ -2,21 +2,28 @@
 
 Headline metric (BASELINE.json): "train images/sec (dinob 1024px bf16) at 1/2/4/8 GPU; infer masks/sec 1GPU".
 Default workload = configs[2]: synth_sod train model=dinob, 1024x1024, bs=16 per GPU, bf16, forward +
-focal_iou loss + backward + fused AdamW, synthetic on-device data.  --gpus N runs data-parallel over
-RCCL (launched by torch.distributed.run, one rank per GPU), per-GPU batch fixed ("weak" scaling).
---mode infer measures configs[1] (bs=8 eval forward, masks/s).
+focal_iou loss + backward + fused AdamW (which invalidates and re-packs the kernel-layout weights every
+step), synthetic on-device data.  --gpus N runs data-parallel over RCCL, one rank per GPU, per-GPU batch
+fixed ("weak" scaling): when the driver already launched the ranks (WORLD_SIZE in the environment) each
+rank joins; a bare `python bench.py --gpus N` spawns `torch.distributed.run` itself (a child process,
+started before anything touches the GPU) and exits with its status.  --mode infer measures configs[1].
 
-`roofline`: the dominant kernel's ALGORITHMIC FLOPs per launch / its mean launch time measured with
-HIP events around every launch inside the timed region.
-`cpu_baseline`: the oracle (oracle/s3od_oracle.py, the reference's CPU fp32 path restated) timed on
-this host's cores on a bounded sample (rank 0, N=1 only).
+`roofline`: the dominant C-ABI entry point of the step (largest summed GPU time in an untimed profiling
+pass) is timed live with HIP events on its launch stream around every call inside the timed region;
+`achieved` = its ALGORITHMIC work (tools/costs.py, from the call arguments) / that time.
+`breakdown`: per-class table (GEMM / attention / memory-bound) from a separate 2-step pass with every
+entry timed, plus the whole-step MFMA fraction and the ViT-encoder ("attention block") fraction.
+`cpu_baseline`: the oracle (oracle/s3od_oracle.py, the reference's CPU fp32 path restated) on this
+host's cores (rank 0, N=1 only): 1 warm-up + --cpu-iters timed iterations of one image (BASELINE.md
+"CPU-baseline plan"); C2 / C5 baselines ride in the `infer` / `infer_2048` objects.
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -29,6 +36,10 @@ sys.path.insert(0, str(ROOT))
 
 PEAK_BF16 = 2.5e15      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32 = 157.3e12     # f32 MFMA
+PEAK_HBM = 8.0e12
+TRAIN_TF_PER_IMG = {1024: 6.826e12}                 # SURVEY §8(d) / BASELINE.md (required work)
+INFER_TF_PER_IMG = {1024: 2.2768e12, 2048: 15.908e12}
+METRIC = "train images/sec (dinob 1024px bf16) at 1/2/4/8 GPU; infer masks/sec 1GPU"
 
 
 def synthetic_batch(B, S, seed, dev):
@@ -51,15 +62,39 @@ def synthetic_batch(B, S, seed, dev):
     return x.contiguous(), masks.contiguous()
 
 
-def attn_flops(B, S):
-    N = (S // 16) ** 2 + 5
-    return 4.0 * B * 12 * N * N * 64           # QK^T + PV per layer launch
+def log(msg):
+    """Progress on stderr (keeps long CPU-baseline phases visibly alive; stdout carries only the JSON line)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def cpu_baseline(S, mode, threads):
-    """Oracle (reference CPU path restated in PyTorch fp32) on one image."""
+# ------------------------------------------------------------------------------------ CPU baseline
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads():
+    """BASELINE.md asks for os.cpu_count() threads; on the shared GPU box that count is the whole
+    machine while the job's share is OMP_NUM_THREADS (16), so use the smaller of the two."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return min(n, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else n
+
+
+def cpu_baseline(S, mode, iters):
+    """Oracle (reference CPU path restated in PyTorch fp32) on one image: 1 warm-up + `iters` timed."""
     from oracle import s3od_oracle as O
     from s3od_amd.weights import synthetic_state_dict
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     sd = {k: torch.from_numpy(v) for k, v in synthetic_state_dict(0).items()}
     x, masks = synthetic_batch(1, S, 123, "cpu")
@@ -76,21 +111,97 @@ def cpu_baseline(S, mode, threads):
         def run():
             with torch.no_grad():
                 O.forward(x, sd)
-    t0 = time.perf_counter()
-    run()                        # warm-up (also counted into the budget)
-    t1 = time.perf_counter()
-    n = 1 if (t1 - t0) > 8 else 2
-    t2 = time.perf_counter()
-    for _ in range(n):
+    log(f"cpu baseline {mode} {S}x{S}: warm-up ({threads} threads)")
+    run()                        # warm-up
+    ts = []
+    for it in range(iters):
+        t0 = time.perf_counter()
         run()
-    dt = (time.perf_counter() - t2) / n
-    return {"value": round(1.0 / dt, 4), "unit": "images/s" if mode == "train" else "masks/s", "cores": threads,
-            "kind": "port", "sample": f"1 image {S}x{S}, {'fwd+focal_iou loss+bwd' if mode == 'train' else 'eval fwd'}, "
-                                      f"fp32 oracle (oracle/s3od_oracle.py), {n} timed iter after 1 warm-up, {threads} threads"}
+        ts.append(time.perf_counter() - t0)
+        log(f"cpu baseline {mode} {S}x{S}: iteration {it + 1}/{iters} {ts[-1]:.2f} s")
+    dt = sum(ts) / len(ts)
+    what = "fwd+focal_iou loss+bwd (no optimizer)" if mode == "train" else "eval fwd"
+    return {"value": round(1.0 / dt, 5), "unit": "images/s" if mode == "train" else "masks/s", "cores": threads,
+            "kind": "port", "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count(),
+            "iter_s": [round(t, 3) for t in ts],
+            "sample": f"1 image {S}x{S}, {what}, fp32 oracle (oracle/s3od_oracle.py), 1 warm-up + {iters} timed "
+                      f"iterations, {threads} threads"}
 
 
-def infer_rate(model, B, S, steps, warmup, dev):
+# ------------------------------------------------------------------------------------ profiling helpers
+def _drain(timers):
+    """{name: [(e0, e1, (kind, work), phase)]} -> per-call records (name, ms, kind, work, phase)."""
+    torch.cuda.synchronize()
+    rec = []
+    for name, evs in timers.items():
+        for e0, e1, c, ph in evs:
+            kind, work = c if c is not None else ("other", 0.0)
+            rec.append((name, e0.elapsed_time(e1), kind, work, ph))
+    return rec
+
+
+def breakdown(step, steps, peak):
+    from s3od_amd import _lib
+    from tools.costs import cost, klass
+    lib = _lib.lib()
+    lib.cost = cost
+    lib.timers = {"*": []}
+    for _ in range(steps):
+        step()
+    timers = lib.timers
+    lib.timers = {}
+    timers.pop("*", None)
+    rec = _drain(timers)
+    by_entry, by_class = {}, {}
+    for name, ms, kind, work, ph in rec:
+        for key, tab in ((name, by_entry), (klass(name), by_class)):
+            d = tab.setdefault(key, {"ms": 0.0, "calls": 0, "kind": kind, "work": 0.0})
+            d["ms"] += ms; d["calls"] += 1; d["work"] += work
+    tot = sum(d["ms"] for d in by_entry.values())
+
+    def fmt(d):
+        o = {"ms_per_step": round(d["ms"] / steps, 3), "pct": round(100 * d["ms"] / tot, 1), "calls_per_step": d["calls"] // steps}
+        if d["kind"] == "mfma" and d["ms"] > 0:
+            o["TFLOP/s"] = round(d["work"] / d["ms"] / 1e9, 1)
+            o["frac_of_peak"] = round(d["work"] / (d["ms"] * 1e-3) / peak, 3)
+        elif d["kind"] == "hbm" and d["ms"] > 0 and d["work"] > 0:
+            o["GB/s"] = round(d["work"] / d["ms"] / 1e6, 1)
+            o["frac_of_hbm"] = round(d["work"] / (d["ms"] * 1e-3) / PEAK_HBM, 3)
+        return o
+    mf = sum(w for _, _, k, w, _ in rec if k == "mfma")
+    enc = [(ms, k, w) for _, ms, k, w, ph in rec if ph == "encoder"]
+    enc_ms = sum(ms for ms, _, _ in enc)
+    enc_fl = sum(w for ms, k, w in enc if k == "mfma")
+    dom = max(by_entry.items(), key=lambda kv: kv[1]["ms"])[0]
+    return dom, {
+        "steps": steps, "kernel_ms_per_step": round(tot / steps, 3),
+        "algorithmic_TF_per_step": round(mf / steps / 1e12, 3),
+        "kernel_busy_mfma_frac": round(mf / (tot * 1e-3) / peak, 3),
+        "vit_encoder": {"ms_per_step": round(enc_ms / steps, 3), "TF_per_step": round(enc_fl / steps / 1e12, 3),
+                        "frac_of_peak": round(enc_fl / (enc_ms * 1e-3) / peak, 3) if enc_ms else None,
+                        "note": "A4-A6 (11 ViT layers + patch embed) FLOPs over the time of every kernel the encoder "
+                                "launches, memory-bound ones included (north_star 'attention block' target >= 0.40)"},
+        "by_class": {k: fmt(v) for k, v in sorted(by_class.items(), key=lambda kv: -kv[1]["ms"])},
+        "by_entry": {k: fmt(v) for k, v in sorted(by_entry.items(), key=lambda kv: -kv[1]["ms"])[:16]},
+    }
+
+
+def pmc_traffic(entry):
+    """HBM bytes per launch of `entry`'s main kernel from the newest committed rocprofv3 PMC summary
+    (profiles/<tag>_pmc.json, written by tools/collect_profiles.py from separate --pmc passes), or None."""
+    for f in sorted((ROOT / "profiles").glob("*_pmc.json"), reverse=True):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("entry") == entry:
+            return {"bytes": d["traffic_bytes_per_launch"], "source": f"profiles/{f.name}", "kernel": d.get("kernel")}
+    return None
+
+
+def infer_rate(model, B, S, steps, warmup, dev, cpu_iters):
     """Eval-forward throughput (configs[1] / configs[4]): one selected mask per image -> masks/s."""
+    log(f"inference bs={B} {S}x{S}")
     x, _ = synthetic_batch(B, S, 7, dev)
     was_training = model.training
     model.eval()
@@ -106,22 +217,35 @@ def infer_rate(model, B, S, steps, warmup, dev):
     model.train(was_training)
     ok = bool(torch.isfinite(out).all().item())
     del out, x
-    return {"value": round(B * steps / dt, 3), "unit": "masks/s", "ms_per_step": round(dt / steps * 1e3, 3),
-            "batch": B, "image_size": S, "steps": steps, "warmup": warmup, "finite": ok}
-
-
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
-    (profiles/<tag>_pmc.json, written by tools/collect_profiles.py), or None."""
-    files = sorted((ROOT / "profiles").glob("*_pmc.json"))
-    for f in reversed(files):
+    value = B * steps / dt
+    res = {"value": round(value, 3), "unit": "masks/s", "ms_per_step": round(dt / steps * 1e3, 3),
+           "batch": B, "image_size": S, "steps": steps, "warmup": warmup, "finite": ok,
+           "mfma_frac": round(value * INFER_TF_PER_IMG[S] / PEAK_BF16, 4)}
+    if cpu_iters > 0:
         try:
-            d = json.load(open(f))
-        except Exception:
-            continue
-        if d.get("kernel") == kernel:
-            return {"bytes": d["traffic_bytes_per_launch"], "source": f"profiles/{f.name}"}
-    return None
+            res["cpu_baseline"] = cpu_baseline(S, "infer", cpu_iters)
+        except Exception as e:  # reported, never fatal for the GPU number
+            res["cpu_baseline"] = {"value": None, "error": repr(e)[:200]}
+    return res
+
+
+# ------------------------------------------------------------------------------------ launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` without a launcher: run N ranks under torch.distributed.run as a
+    child process (no exec, no GPU touched in this process) and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "bench.py")] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -134,21 +258,26 @@ def main():
     ap.add_argument("--size", type=int, default=1024)
     ap.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--no-infer", action="store_true", help="skip the secondary inference lines (train mode)")
+    ap.add_argument("--no-breakdown", action="store_true", help="skip the per-class profiling pass")
     ap.add_argument("--ddp", action="store_true",
                     help="use the RCCL data-parallel path even at world size 1 (rehearsal on one GPU)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and world != args.gpus and rank == 0:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; using the launcher's world size", file=sys.stderr)
     use_dist = world > 1 or args.ddp
-    if use_dist:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if use_dist:
+        dist.init_process_group("nccl", device_id=dev)
 
     from s3od_amd.model import DPTSegmentation
     from s3od_amd.loss import LossModule, FOCAL_IOU
@@ -158,11 +287,10 @@ def main():
     B = args.batch or (16 if args.mode == "train" else 8)
     S = args.size
     model = DPTSegmentation(compute_dtype=args.dtype).to(dev)
-    sync = None
     if use_dist:
         from s3od_amd.ddp import GradSync, broadcast_parameters
         broadcast_parameters(model)
-        sync = GradSync(model)
+        GradSync(model)
     x, masks = synthetic_batch(B, S, 1000 + rank, dev)
 
     if args.mode == "train":
@@ -184,11 +312,20 @@ def main():
             with torch.no_grad():
                 return model(x)["pred_masks"]
 
+    peak = PEAK_BF16 if args.dtype == "bf16" else PEAK_F32
+    log(f"{args.mode} bs={B} {S}x{S} {args.dtype}: warm-up")
     for _ in range(args.warmup):
         step()
+    # untimed profiling pass: which entry point dominates (and the per-class table)
+    bd = None
+    dom = "s3od_attn_bwd" if args.mode == "train" else "s3od_attn_fwd"
+    if not args.no_breakdown:
+        dom, bd = breakdown(step, 2, peak)
     torch.cuda.synchronize()
-    dom = "s3od_attn_fwd"
+    log(f"timed region: {args.steps} steps, roofline entry {dom}")
+    from tools.costs import cost
     lib = _lib.lib()
+    lib.cost = cost
     lib.timers = {dom: []}
     if use_dist:
         dist.barrier()
@@ -204,45 +341,59 @@ def main():
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    ev = lib.timers.pop(dom)
+    timers = lib.timers
     lib.timers = {}
-    kms = sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
+    rec = _drain(timers)
+    kms = sum(r[1] for r in rec) / max(len(rec), 1)
+    work = sum(r[3] for r in rec) / max(len(rec), 1)
+    kind = rec[0][2] if rec else "mfma"
     ok = bool(torch.isfinite(last.float()).all().item())
 
     if rank == 0:
         total = B * world * args.steps
         value = total / el
-        metric = ("train images/sec (dinob 1024px bf16) at 1/2/4/8 GPU; infer masks/sec 1GPU")
         unit = "images/s" if args.mode == "train" else "masks/s"
-        peak = PEAK_BF16 if args.dtype == "bf16" else PEAK_F32
-        achieved = attn_flops(B, S) / (kms * 1e-3) if kms > 0 else 0.0
-        tr = pmc_traffic("attn_fwd_kernel") if (B == 16 and S == 1024 and args.dtype == "bf16") else None
+        achieved = work / (kms * 1e-3) if kms > 0 else 0.0
+        pk = peak if kind == "mfma" else PEAK_HBM
+        tr = pmc_traffic(dom) if (B == 16 and S == 1024 and args.dtype == "bf16" and args.mode == "train") else None
+        per_img = (TRAIN_TF_PER_IMG if args.mode == "train" else INFER_TF_PER_IMG).get(S)
         res = {
-            "metric": metric, "value": round(value, 3), "unit": unit, "n_gpus": world, "steps": args.steps,
+            "metric": METRIC, "value": round(value, 3), "unit": unit, "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (seeded uint8 images, ImageNet-normalised; 1-3 ellipse masks), deterministic synthetic weights",
             "config": {"workload": ("synth_sod train model=dinob 1024px bs=16/GPU fwd+focal_iou loss+bwd+AdamW"
                                     if args.mode == "train" else "dinob inference bs=8 1024x1024 eval forward"),
                        "model": "dinob (DINOv3 ViT-B/16 + DPT + 3-mask head)", "global_batch": B * world,
-                       "image_size": S, "parallelism": f"dp{world}"},
-            "roofline": {"kernel": "attn_fwd_kernel (flash attention fwd, 1 launch per ViT layer)", "bound": "mfma",
-                         "achieved": round(achieved / 1e12, 2), "peak": round(peak / 1e12, 1), "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4), "traffic": round(tr["bytes"]) if tr else None,
-                         "traffic_unit": "bytes/launch (FETCH_SIZE*2 + WRITE_SIZE, gfx950-corrected)",
+                       "image_size": S, "parallelism": f"dp{world}",
+                       "rccl_world_size": dist.get_world_size() if use_dist else 1},
+            "roofline": {"entry": dom, "bound": "mfma" if kind == "mfma" else "hbm",
+                         "achieved": round(achieved / (1e12 if kind == "mfma" else 1e9), 2),
+                         "peak": round(pk / (1e12 if kind == "mfma" else 1e9), 1),
+                         "unit": "TFLOP/s" if kind == "mfma" else "GB/s",
+                         "frac": round(achieved / pk, 4),
+                         "traffic": round(tr["bytes"]) if tr else None,
+                         "traffic_unit": "HBM bytes/launch of the entry's main kernel (rocprofv3 FETCH_SIZE*2 + WRITE_SIZE, "
+                                         "gfx950-corrected, separate --pmc passes)",
                          "traffic_source": tr["source"] if tr else None,
-                         "flops_per_launch": attn_flops(B, S), "mean_launch_ms": round(kms, 4), "launches": len(ev)},
+                         "work_per_launch": work, "mean_launch_ms": round(kms, 4), "launches": len(rec),
+                         "note": "dominant C-ABI entry point by summed GPU time; HIP events on its launch stream around "
+                                 "every call in the timed region; work = algorithmic (tools/costs.py)"},
+            "mfma_frac_step": round(value / world * per_img / peak, 4) if per_img else None,
             "finite": ok,
         }
+        if bd is not None:
+            res["breakdown"] = bd
         if args.mode == "train" and world == 1 and not args.no_infer and args.dtype == "bf16":
+            ci = 0 if args.no_cpu_baseline else args.cpu_iters
             # the metric's second half ("infer masks/sec 1GPU"): configs[1] and configs[4]
-            res["infer"] = dict(infer_rate(model, 8, 1024, 10, 3, dev),
+            res["infer"] = dict(infer_rate(model, 8, 1024, 10, 3, dev, ci),
                                 config="dinob inference bs=8 1024x1024 eval forward (configs[1])")
-            res["infer_2048"] = dict(infer_rate(model, 4, 2048, 4, 2, dev),
+            res["infer_2048"] = dict(infer_rate(model, 4, 2048, 4, 2, dev, ci),
                                      config="high-res 2048x2048 eval forward bs=4 (configs[4])")
         if not args.no_cpu_baseline and world == 1:
             try:
-                res["cpu_baseline"] = cpu_baseline(S, args.mode, args.cpu_threads)
+                res["cpu_baseline"] = cpu_baseline(S, args.mode, args.cpu_iters)
             except Exception as e:  # reported, never fatal for the GPU number
                 res["cpu_baseline"] = {"value": None, "error": repr(e)[:200]}
         print(json.dumps(res), flush=True)

@@ -100,7 +100,7 @@ def encoder_taps(x, sd, rope_rescale=None):
     indices [2,5,8,11] (src/s3od/model.py:36-40,62-86) and drops 1+4 prefix tokens.
     Layer 11 and the final norm never reach the outputs, so they are not run."""
     ph, pw = x.shape[-2] // PATCH, x.shape[-1] // PATCH
-    cos, sin = rope_cos_sin(ph, pw, rope_rescale)
+    cos, sin = (t.to(x.device) for t in rope_cos_sin(ph, pw, rope_rescale))
     h = patch_embed(x, sd)
     taps = []
     for i in range(max(TAPS)):
@@ -211,7 +211,7 @@ def _gauss_window(ws=11, sigma=1.5):
 
 def ssim_loss(img1, img2, ws=11):
     """loss.py:34-76 with reduction='none'."""
-    w = _gauss_window(ws).to(img1.dtype)
+    w = _gauss_window(ws).to(device=img1.device, dtype=img1.dtype)
     mu1 = F.conv2d(img1, w, padding=ws // 2)
     mu2 = F.conv2d(img2, w, padding=ws // 2)
     mu1_sq, mu2_sq, mu12 = mu1.pow(2), mu2.pow(2), mu1 * mu2
@@ -245,7 +245,7 @@ def multi_mask_loss(outputs, masks, epoch=0, cfg=FOCAL_IOU):
         union = (tf ** 2).reshape(B * M, 1, -1).sum(2) + (pf ** 2).reshape(B * M, 1, -1).sum(2) - inter
         ious = ((inter + 1e-6) / (union + 1e-6)).mean(1).reshape(B, M)
     best = ious.argmax(dim=1)
-    total = torch.zeros(())
+    total = torch.zeros((), device=logits.device)
     parts = {"best_iou": ious.max(dim=1)[0].mean(), "gt_ious": ious}
     for name, w, kind in cfg["components"]:
         if kind == "focal":

@@ -56,7 +56,9 @@ class _Lib:
         self.lib = ctypes.CDLL(str(LIB_PATH))
         self.decls = parse_header()
         self.fns = {}
-        self.timers = {}     # name -> list of (start, end) events recorded around each call
+        self.timers = {}     # name -> list of (start, end, args, phase) recorded around each call
+        self.phase = None    # set by the engine ("encoder" / "decoder" / "prepare") for the bench breakdown
+        self.cost = None     # optional fn(name, args) -> (kind, work), evaluated at call time (no tensor kept alive)
         for name, (ret, types) in self.decls.items():
             fn = getattr(self.lib, name)
             fn.argtypes = [_CT[t] for t in types]
@@ -80,13 +82,19 @@ class _Lib:
                     cargs.append(int(a))
             else:
                 cargs.append(a)
-        tm = self.timers.get(name) if self.timers else None
+        tm = None
+        if self.timers:
+            tm = self.timers.get(name)
+            if tm is None and "*" in self.timers:       # time every entry point (bench breakdown pass)
+                tm = self.timers.setdefault(name, [])
         if tm is not None:
+            # events on the stream the kernel is launched on (the last argument of every entry)
+            st = torch.cuda.ExternalStream(cargs[-1]) if types[-1] == "void*" and cargs[-1] else torch.cuda.current_stream()
             e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
-            e0.record()
+            e0.record(st)
             rc = fn(*cargs)
-            e1.record()
-            tm.append((e0, e1))
+            e1.record(st)
+            tm.append((e0, e1, self.cost(name, args) if self.cost else None, self.phase))
         else:
             rc = fn(*cargs)
         if rc != 0:

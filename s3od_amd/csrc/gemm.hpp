@@ -155,16 +155,21 @@ template <typename T, int R, int NW = GEMM_WAVES> struct DenseKC {          // X
   static constexpr bool KCL = true, RELU = false;
   typedef KCGeom<T, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* p; long ld; int nrows, K; int relu;
+  const T* pb; unsigned long nb;           // this block's row window (descriptor rebased per block)
   unsigned vo[NIW]; int kel[NIW];
-  HD unsigned long bytes() const { return ((unsigned long)(nrows - 1) * ld + K) * sizeof(T); }
+  // the descriptor only ever spans the R rows of one block, so the tensor itself may exceed 4 GiB
+  HD unsigned long bytes() const { return ((unsigned long)(R - 1) * ld + K) * sizeof(T); }
   HD bool buf_ok() const { return bytes() < BUF_MAX && (unsigned long)K * sizeof(T) < 0x4000000ul; }
   DEV void setup(int t0, int tid) {
     const int lane = tid & 63, wave = wave_id();
+    const int rem = nrows - t0;
+    pb = p + (long)t0 * ld;
+    nb = rem > 0 ? ((unsigned long)(min(rem, R) - 1) * ld + K) * sizeof(T) : 0;
 #pragma unroll
     for (int i = 0; i < NIW; i++) {
-      int r = t0 + G::row(wave, i, lane);
+      int r = G::row(wave, i, lane);
       kel[i] = G::kel(wave, i, lane);
-      vo[i] = r < nrows ? (unsigned)(((long)r * ld + kel[i]) * sizeof(T)) : BUF_OOB;
+      vo[i] = r < rem ? (unsigned)(((long)r * ld + kel[i]) * sizeof(T)) : BUF_OOB;
     }
   }
   DEV void issue(int kt, char* tile) { issue_to(kt, DmaSink{tile + wave_id() * NIW * 1024}); }
@@ -176,7 +181,7 @@ template <typename T, int R, int NW = GEMM_WAVES> struct DenseKC {          // X
     for (int i = 0; i < NIW; i++) *(u32x4_t*)(b + i * 1024) = regs[i];
   }
   template <class SK> DEV void issue_to(int kt, SK sk) {
-    const auto rs = make_rsrc(p, bytes());
+    const auto rs = make_rsrc(pb, nb);
     const unsigned adv = (unsigned)(kt * BK * sizeof(T));
     if ((kt + 1) * BK > K) {          // K tail (uniform branch)
 #pragma unroll
@@ -194,7 +199,9 @@ template <typename T, int R, int NW = GEMM_WAVES> struct DenseMC {          // X
   const T* p; long ld; int K, ncols;
   int relu = 0;
   unsigned vo[NIW]; int kr[NIW]; bool cv[NIW];
-  HD unsigned long bytes() const { return ((unsigned long)(K - 1) * ld + ncols) * sizeof(T); }
+  // the descriptor is rebased to each K tile's first row: only BK rows need to be addressable
+  HD unsigned long total() const { return ((unsigned long)(K - 1) * ld + ncols) * sizeof(T); }
+  HD unsigned long bytes() const { return ((unsigned long)BK * ld) * sizeof(T); }
   HD bool buf_ok() const { return bytes() < BUF_MAX; }
   DEV void setup(int t0, int tid) {
     const int lane = tid & 63, wave = wave_id();
@@ -215,17 +222,25 @@ template <typename T, int R, int NW = GEMM_WAVES> struct DenseMC {          // X
     for (int i = 0; i < NIW; i++) *(u32x4_t*)(b + i * 1024) = regs[i];
   }
   template <class SK> DEV void issue_to(int kt, SK sk) {
-    const auto rs = make_rsrc(p, bytes());
-    const unsigned adv = (unsigned)((long)kt * BK * ld * sizeof(T));
+    const long e0 = (long)kt * BK * ld;
+    const auto rs = make_rsrc(p + e0, total() - (unsigned long)e0 * sizeof(T));
     if ((kt + 1) * BK > K) {          // K tail (uniform branch)
 #pragma unroll
-      for (int i = 0; i < NIW; i++) sk(i, rs, cv[i] && kt * BK + kr[i] < K ? vo[i] + adv : BUF_OOB);
+      for (int i = 0; i < NIW; i++) sk(i, rs, cv[i] && kt * BK + kr[i] < K ? vo[i] : BUF_OOB);
       return;
     }
 #pragma unroll
-    for (int i = 0; i < NIW; i++) sk(i, rs, cv[i] ? vo[i] + adv : BUF_OOB);
+    for (int i = 0; i < NIW; i++) sk(i, rs, cv[i] ? vo[i] : BUF_OOB);
   }
 };
+
+// Image window of a gather: a block (or K tile) whose rows cover pixels [first, last] of a batch of
+// images of `hw` pixels reads images first/hw .. last/hw only.  The descriptor is rebased to the
+// first of them, so only that window (not the whole batch) must stay below BUF_MAX.
+HD inline unsigned long img_window_bytes(int rows, int hw, int B, unsigned long img_bytes) {
+  long n = (long)(rows - 1) / hw + 2;
+  return (unsigned long)(n < B ? n : B) * img_bytes;
+}
 
 // Incremental K-tile -> (tap, channel base) walker for gathers whose K is tap-major with
 // SC % BK == 0: a whole K tile then lies inside one tap, so tap/channel are wave-uniform.
@@ -258,15 +273,20 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Con
   static constexpr bool KCL = true, RELU = RELU_;
   typedef KCGeom<T, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* x; ConvGeo g; int M; int relu;
+  const T* xb; unsigned long nb;          // image window of this block (rebased descriptor)
   int iy0[NIW], ix0[NIW], pix0[NIW];      // top-left input pixel (may be outside) and its element offset + kel
   int kl[NIW];
   unsigned base[NIW];
   TapWalk tw;
-  HD unsigned long bytes() const { return (unsigned long)g.B * g.SH * g.SW * g.SC * sizeof(T); }
+  HD unsigned long img_bytes() const { return (unsigned long)g.SH * g.SW * g.SC * sizeof(T); }
+  HD unsigned long bytes() const { return img_window_bytes(R, g.RH * g.RW, g.B, img_bytes()); }
   HD bool buf_ok() const { return bytes() < BUF_MAX && g.SC >= BK; }
   DEV void setup(int t0, int tid) {
     const int lane = tid & 63, wave = wave_id();
     int hw = g.RH * g.RW;
+    const int b0 = min(t0, M - 1) / hw, b1 = min(t0 + R - 1, M - 1) / hw;
+    xb = x + (long)b0 * g.SH * g.SW * g.SC;
+    nb = (unsigned long)(b1 - b0 + 1) * img_bytes();
 #pragma unroll
     for (int i = 0; i < NIW; i++) {
       int m = t0 + G::row(wave, i, lane);
@@ -275,7 +295,7 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Con
       if (m < M) {
         int b = m / hw; int r = m - b * hw; int oy = r / g.RW;
         iy0[i] = oy * g.s - g.p; ix0[i] = (r - oy * g.RW) * g.s - g.p;
-        pix0[i] = ((b * g.SH + iy0[i]) * g.SW + ix0[i]) * g.SC + kel;
+        pix0[i] = (((b - b0) * g.SH + iy0[i]) * g.SW + ix0[i]) * g.SC + kel;
       } else { iy0[i] = -0x4000000; ix0[i] = 0; pix0[i] = 0; }
     }
     tw = TapWalk{};
@@ -289,7 +309,7 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Con
     for (int i = 0; i < NIW; i++) *(u32x4_t*)(b + i * 1024) = regs[i];
   }
   template <class SK> DEV void issue_to(int kt, SK sk) {
-    const auto rs = make_rsrc(x, bytes());
+    const auto rs = make_rsrc(xb, nb);
     if (g.SC % BK) {                 // channels not a multiple of BK: per-lane tap (rare shapes)
       tw.step_any(kt, BK, g.SC, g.KW);
       int th1, tw1; tw.next_tap(g.KW, th1, tw1);
@@ -327,14 +347,19 @@ template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradA {
   typedef KCGeom<T, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* dy; ConvGeo g; int M;
   int relu = 0;
+  const T* yb; unsigned long nb;          // image window of this block (rebased descriptor)
   int ry[NIW], rx[NIW], pix0[NIW], kl[NIW];
   unsigned base[NIW];
   TapWalk tw;
-  HD unsigned long bytes() const { return (unsigned long)g.B * g.SH * g.SW * g.SC * sizeof(T); }
+  HD unsigned long img_bytes() const { return (unsigned long)g.SH * g.SW * g.SC * sizeof(T); }
+  HD unsigned long bytes() const { return img_window_bytes(R, g.RH * g.RW, g.B, img_bytes()); }
   HD bool buf_ok() const { return bytes() < BUF_MAX && g.SC >= BK; }
   DEV void setup(int t0, int tid) {
     const int lane = tid & 63, wave = wave_id();
     int hw = g.RH * g.RW;
+    const int b0 = min(t0, M - 1) / hw, b1 = min(t0 + R - 1, M - 1) / hw;
+    yb = dy + (long)b0 * g.SH * g.SW * g.SC;
+    nb = (unsigned long)(b1 - b0 + 1) * img_bytes();
 #pragma unroll
     for (int i = 0; i < NIW; i++) {
       int m = t0 + G::row(wave, i, lane);
@@ -343,7 +368,7 @@ template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradA {
       if (m < M) {
         int b = m / hw; int r = m - b * hw; int yy = r / g.RW;
         ry[i] = yy + g.qy0; rx[i] = (r - yy * g.RW) + g.qx0;
-        pix0[i] = ((b * g.SH + ry[i]) * g.SW + rx[i]) * g.SC + kel;
+        pix0[i] = (((b - b0) * g.SH + ry[i]) * g.SW + rx[i]) * g.SC + kel;
       } else { ry[i] = -0x4000000; rx[i] = 0; pix0[i] = 0; }
     }
     tw = TapWalk{};
@@ -357,7 +382,7 @@ template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradA {
     for (int i = 0; i < NIW; i++) *(u32x4_t*)(b + i * 1024) = regs[i];
   }
   template <class SK> DEV void issue_to(int kt, SK sk) {
-    const auto rs = make_rsrc(dy, bytes());
+    const auto rs = make_rsrc(yb, nb);
     const int TW = g.ntw > 0 ? g.ntw : 1;
     if (g.SC % BK) {                 // channels not a multiple of BK: per-lane tap (rare shapes)
       tw.step_any(kt, BK, g.SC, TW);
@@ -456,7 +481,10 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Wgr
   int kh[NIW], kw[NIW], kr[NIW], cin[NIW]; unsigned lo[NIW]; bool cval[NIW];
   int nk, pb, poy, pox;                         // uniform walker (fast path)
   int qb[NIW], qy[NIW], qx[NIW];                // per-lane walker (generic path)
-  HD unsigned long bytes() const { return (unsigned long)g.B * g.SH * g.SW * g.SC * sizeof(T); }
+  // the descriptor is rebased per K tile to the image of its first pixel (a tile of BK pixels
+  // spans at most BK/hw + 2 images), so the batch itself may exceed 4 GiB
+  HD unsigned long img_bytes() const { return (unsigned long)g.SH * g.SW * g.SC * sizeof(T); }
+  HD unsigned long bytes() const { return img_window_bytes(BK, g.RH * g.RW, g.B, img_bytes()); }
   HD bool buf_ok() const { return bytes() < BUF_MAX; }
   DEV void setup(int t0, int tid) {
     const int lane = tid & 63, wave = wave_id();
@@ -480,14 +508,14 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Wgr
     for (int i = 0; i < NIW; i++) *(u32x4_t*)(b + i * 1024) = regs[i];
   }
   template <class SK> DEV void issue_to(int kt, SK sk) {
-    const auto rs = make_rsrc(x, bytes());
     if (g.RW % BK == 0) {
       if (kt != nk) { int k = kt * BK; int hw = g.RH * g.RW; pb = k / hw; int r = k - pb * hw; poy = r / g.RW; pox = r - poy * g.RW; }
       else { pox += BK; if (pox >= g.RW) { pox = 0; if (++poy >= g.RH) { poy = 0; pb++; } } }
       nk = kt + 1;
       const int iy0 = poy * g.s - g.p, ix0 = pox * g.s - g.p;
       const bool live = pb < g.B;
-      const unsigned uo = (unsigned)((((long)pb * g.SH + iy0) * g.SW + ix0) * g.SC * (long)sizeof(T));
+      const auto rs = make_rsrc(x + (long)(live ? pb : 0) * g.SH * g.SW * g.SC, img_bytes());
+      const unsigned uo = (unsigned)(((long)iy0 * g.SW + ix0) * g.SC * (long)sizeof(T));
       const bool interior = iy0 >= 0 && iy0 + g.KH <= g.SH && ix0 >= 0 && ix0 + (BK - 1) * g.s + g.KW <= g.SW;
       if (live && interior) {
 #pragma unroll
@@ -502,9 +530,11 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Wgr
       }
       return;
     }
-    // generic: per-lane pixel walker
+    // generic: per-lane pixel walker, descriptor rebased to the image of the tile's first pixel
+    const int hw = g.RH * g.RW;
+    const int b0 = min(kt * BK / hw, g.B - 1);
+    const auto rs = make_rsrc(x + (long)b0 * g.SH * g.SW * g.SC, (unsigned long)(g.B - b0) * img_bytes());
     if (kt != nk) {
-      const int hw = g.RH * g.RW;
 #pragma unroll
       for (int i = 0; i < NIW; i++) {
         int k = kt * BK + kr[i];
@@ -517,7 +547,7 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Wgr
     for (int i = 0; i < NIW; i++) {
       int iy = qy[i] * g.s - g.p + kh[i], ix = qx[i] * g.s - g.p + kw[i];
       bool ok = cval[i] && qb[i] < g.B && (unsigned)iy < (unsigned)g.SH && (unsigned)ix < (unsigned)g.SW;
-      unsigned v = (unsigned)(((((long)qb[i] * g.SH + iy) * g.SW + ix) * g.SC + cin[i]) * (long)sizeof(T));
+      unsigned v = (unsigned)(((((long)(qb[i] - b0) * g.SH + iy) * g.SW + ix) * g.SC + cin[i]) * (long)sizeof(T));
       sk(i, rs, ok ? v : BUF_OOB);
       qx[i] += BK;
       while (qx[i] >= g.RW) { qx[i] -= g.RW; if (++qy[i] >= g.RH) { qy[i] = 0; qb[i]++; } }

@@ -84,14 +84,15 @@ DEV int aa_weights(int i, int in, int out, float* w, int maxw) {
   return xmin | (xsize << 20);
 }
 
-// pass 1: sigmoid + crop + horizontal resample: [3][S][S] logits -> tmp [3][h][W0]
-__global__ void post_h_kernel(const float* __restrict__ logits, int S, int pad_h, int pad_w, int h, int w, int W0, float* __restrict__ tmp) {
+// pass 1: sigmoid + crop + horizontal resample: [3][LH][LW] logits -> tmp [3][h][W0]
+__global__ void post_h_kernel(const float* __restrict__ logits, int LH, int LW, int pad_h, int pad_w, int h, int w, int W0,
+                              float* __restrict__ tmp) {
   int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, c = blockIdx.z;
   if (x >= W0) return;
   float wt[64];
   int r = aa_weights(x, w, W0, wt, 64);
   int xmin = r & 0xFFFFF, xs = r >> 20;
-  const float* row = logits + ((long)c * S + (pad_h + y)) * S + pad_w;
+  const float* row = logits + ((long)c * LH + (pad_h + y)) * LW + pad_w;
   float acc = 0.f;
   for (int j = 0; j < xs; j++) acc += wt[j] * (1.f / (1.f + expf(-row[xmin + j])));
   tmp[((long)c * h + y) * W0 + x] = acc;
@@ -121,12 +122,14 @@ int s3od_preprocess(const void* img, int H0, int W0, int new_h, int new_w, int p
   return s3od_check_launch("preprocess");
 }
 
-// logits: fp32 [3][S][S] (one image); tmp: fp32 [3][h][W0]; out: fp32 [3][H0][W0]
-int s3od_sigmoid_unpad_resize(const float* logits, int S, int pad_h, int pad_w, int h, int w, int H0, int W0,
+// logits: fp32 [3][LH][LW] (one image; LH x LW = S x S, or S x 16*floor(new_w/16) for the
+// reference's unpadded Quirk-2 input); tmp: fp32 [3][h][W0]; out: fp32 [3][H0][W0]
+int s3od_sigmoid_unpad_resize(const float* logits, int LH, int LW, int pad_h, int pad_w, int h, int w, int H0, int W0,
                               float* tmp, float* out, void* stream) {
   S3OD_REQUIRE((float)w / W0 < 32.f && (float)h / H0 < 32.f, "postprocess: downscale factor too large");
+  S3OD_REQUIRE(pad_h + h <= LH && pad_w + w <= LW, "postprocess: crop outside the logits");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(post_h_kernel, dim3(cdiv(W0, 256), h, 3), dim3(256), 0, st, logits, S, pad_h, pad_w, h, w, W0, tmp);
+  hipLaunchKernelGGL(post_h_kernel, dim3(cdiv(W0, 256), h, 3), dim3(256), 0, st, logits, LH, LW, pad_h, pad_w, h, w, W0, tmp);
   hipLaunchKernelGGL(post_v_kernel, dim3(cdiv(W0, 256), H0, 3), dim3(256), 0, st, tmp, h, H0, W0, out);
   return s3od_check_launch("sigmoid_unpad_resize");
 }

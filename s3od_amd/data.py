@@ -104,10 +104,14 @@ def _T(tx, ty):
 class GpuAugment:
     """Callable: list of decoded samples -> device batch dict (see module docstring)."""
 
-    def __init__(self, image_size: int, mode: str = "regular", device=None, seed: int = 0):
+    def __init__(self, image_size: int, mode: str = "regular", device=None, seed: Optional[int] = None):
         self.S, self.mode = int(image_size), mode
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-        self.rng = random.Random(seed)
+        # every data-parallel rank draws its own augmentation stream (the reference seeds each
+        # worker from torch.initial_seed(), which differs per rank / worker)
+        rank = torch.distributed.get_rank() if torch.distributed.is_available() and torch.distributed.is_initialized() else 0
+        base = torch.initial_seed() if seed is None else int(seed)
+        self.rng = random.Random(base * 1000003 + rank)
 
     def sample_params(self, h0: int, w0: int, img: Optional[np.ndarray] = None) -> AugParams:
         S, r = self.S, self.rng

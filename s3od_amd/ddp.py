@@ -6,10 +6,14 @@ The native backward calls ``on_ready(range, flat_slice)`` as soon as a block of 
 gradients is final (seg_head first, then ViT layers 10..0, then the embeddings); each block is
 all-reduced (mean) asynchronously on a dedicated HIP stream so communication overlaps the rest
 of the backward.  ``finish()`` joins the outstanding collectives before the optimizer step.
+``no_sync()`` skips the exchange for gradient-accumulation micro-batches (Lightning's
+``accumulate_grad_batches``, backend/8gpu.yaml:6): the flat buffer keeps summing locally and the
+last micro-batch's backward all-reduces the accumulated sum once.
 Works with gloo on CPU tensors too (tests).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -23,6 +27,7 @@ class GradSync:
         self.backend = dist.get_backend(group)
         self.works = []
         self.stream = None
+        self.enabled = True
         # S3OD_DDP_REHEARSE=1: issue the collectives even at world size 1 (exercises the RCCL
         # stream/event path on a one-GPU box; the mean over one rank is the identity)
         self.rehearse = os.environ.get("S3OD_DDP_REHEARSE", "0") == "1"
@@ -30,8 +35,16 @@ class GradSync:
             model.grad_ready_callback = self.on_ready
             model.grad_finish_callback = self.finish
 
+    @contextlib.contextmanager
+    def no_sync(self):
+        prev, self.enabled = self.enabled, False
+        try:
+            yield
+        finally:
+            self.enabled = prev
+
     def on_ready(self, name, flat_slice):
-        if self.world == 1 and not self.rehearse:
+        if not self.enabled or (self.world == 1 and not self.rehearse):
             return
         if flat_slice.is_cuda:
             if self.stream is None:

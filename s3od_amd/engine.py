@@ -69,6 +69,7 @@ class DPTEngine:
         st = stream()
         dev = next(iter(P.values())).device
         w = {}
+        L.phase = "prepare"
 
         def pack(name, O, I, KH=1, KW=1, out=None):
             out = torch.empty((O, KH, KW, I), dtype=T, device=dev) if out is None else out
@@ -118,6 +119,7 @@ class DPTEngine:
         w["heads2_b"] = torch.cat([P[m + f"mask_heads.{k}.2.bias"] for k in range(3)])
         self.w = w
         self._wkey = key
+        L.phase = None
 
     # ------------------------------------------------------------------ helpers
     def _lin(self, x, w, M, N, K, out, bias=None, scale=None, shift=None, act=ACT_NONE, res1=None, res_f32=False,
@@ -151,6 +153,7 @@ class DPTEngine:
 
     # ------------------------------------------------------------------ encoder
     def encoder_forward(self, x, train=False, rope_rescale=None, ctx=None):
+        lib().phase = "encoder"
         L, P, W8, dt, T = lib(), self.p, self.w, self.dt, self.tdt
         st = stream()
         B, _, Hh, Ww = x.shape
@@ -238,7 +241,8 @@ class DPTEngine:
         bn2 = self._bn_train(z2["stats"], npix, q + "bn2")
         out = torch.empty_like(z2["z"])
         L("s3od_affine_act", self.dt, z2["z"], bn2["scale"], bn2["shift"], 0, x, x0, out, out.numel(), 256, st)
-        ctx.t[tag] = dict(x=x, z1=z1["z"], a1=a1, z2=z2["z"], bn1=bn1, bn2=bn2, h=h, w=w)
+        if ctx is not None:   # train-mode BN under no_grad: batch statistics, nothing saved
+            ctx.t[tag] = dict(x=x, z1=z1["z"], a1=a1, z2=z2["z"], bn1=bn1, bn2=bn2, h=h, w=w)
         return out
 
     def _conv_bn_train(self, x, wt, B, h, w, bias, relu_in=False):
@@ -278,6 +282,7 @@ class DPTEngine:
         return self._bilinear(c, B, h, w, oh, ow, 256)
 
     def decoder_forward(self, taps, B, ph, pw, train=False, ctx=None):
+        lib().phase = "decoder"
         L, P, W8, dt = lib(), self.p, self.w, self.dt
         st = stream()
         h = "seg_head."
@@ -323,6 +328,7 @@ class DPTEngine:
           logits, hsave, st)
         if ctx is not None:
             ctx.t["head"] = dict(p1=p1, pooled=pooled, hid=hid, oc1=oc1, up=up, c64=c64, hsave=hsave)
+        lib().phase = None
         return {"pred_masks": logits, "pred_iou": iou, "features": p1.permute(0, 3, 1, 2)}
 
     # ------------------------------------------------------------------ full forward
@@ -330,6 +336,9 @@ class DPTEngine:
         """x: [B,3,H,W] fp32 CUDA (normalised image).  Returns the reference output dict."""
         if x.dtype != torch.float32:
             x = x.float()
+        Hh, Ww = x.shape[2], x.shape[3]
+        if Hh % 16 or Ww % 16:   # the stride-16 patch conv never reads the trailing rows / columns
+            x = x[:, :, :16 * (Hh // 16), :16 * (Ww // 16)]
         x = x.contiguous()
         self.prepare()
         taps, (B, ph, pw, Nt) = self.encoder_forward(x, train, rope_rescale, ctx)
@@ -412,6 +421,7 @@ class DPTEngine:
         return ds, dx1
 
     def decoder_backward(self, ctx, d_logits, d_iou, G):
+        lib().phase = "decoder"
         L, P, W8, dt = lib(), self.p, self.w, self.dt
         st = stream()
         B, ph, pw = ctx.B, ctx.ph, ctx.pw
@@ -479,9 +489,11 @@ class DPTEngine:
         for i, c in enumerate(OUT_CH):
             self._wgrad_lin(dproj[i], dec["taps"][i], c, D_, B * NP, G[h + f"projects.{i}.weight"])
             dtaps.append((dproj[i], c))
+        lib().phase = None
         return dtaps
 
     def encoder_backward(self, ctx, dtaps, G):
+        lib().phase = "encoder"
         L, P, W8, dt, T = lib(), self.p, self.w, self.dt, self.tdt
         st = stream()
         B, ph, pw = ctx.B, ctx.ph, ctx.pw
@@ -545,6 +557,7 @@ class DPTEngine:
         L("s3od_cast_tap", dt, dx, dpatch, B, Nt, NP, st)
         self._colsum(dpatch, B * NP, D_, G[e + "patch_embeddings.bias"])
         self._wgrad_lin(dpatch, ctx.t["cols"], D_, D_, B * NP, G[e + "patch_embeddings.weight"])
+        lib().phase = None
         if self.grad_hook is not None:
             self.grad_hook("embeddings")
 

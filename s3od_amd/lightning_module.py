@@ -56,7 +56,8 @@ def binary_iou(pred, target, thr=0.5):
     t = target.bool()
     inter = (p & t).sum().float()
     union = (p | t).sum().float()
-    return torch.where(union > 0, inter / union.clamp_min(1), torch.ones_like(union))
+    # empty union -> zero_division (0.0, torchmetrics' default; parity unpinned: torchmetrics absent)
+    return torch.where(union > 0, inter / union.clamp_min(1), torch.zeros_like(union))
 
 
 def dice_score(pred, target, thr=0.5):
@@ -83,9 +84,11 @@ class SegmentationLightningModule(_Base):
         t = getattr(self, "trainer", None)
         return getattr(t, "current_epoch", self.current_epoch_) if t is not None else self.current_epoch_
 
-    def log(self, name, value, on_step=True, on_epoch=True, prog_bar=False, sync_dist=False):
+    def log(self, name, value, on_step=True, on_epoch=True, prog_bar=False, sync_dist=False, **kw):
         v = value.detach() if torch.is_tensor(value) else torch.tensor(float(value))
         self._pending[name] = (v.float().reshape(()), sync_dist)
+        if _Base is not nn.Module:   # real Lightning: its logger / ModelCheckpoint(monitor=...) see every key
+            super().log(name, value, on_step=on_step, on_epoch=on_epoch, prog_bar=prog_bar, sync_dist=sync_dist, **kw)
 
     def flush_logs(self):
         """One fused all-reduce (mean) of every sync_dist scalar logged this step."""
@@ -135,8 +138,19 @@ class SegmentationLightningModule(_Base):
         tgt = (targets > 0.5).int()
         return {"iou": binary_iou(best, tgt), "dice": dice_score(best, tgt)}
 
+    def _check_grad_sync(self):
+        """The native backward writes gradients straight into a flat buffer (no AccumulateGrad
+        hooks), so torch/Lightning DDP or FSDP strategies would never all-reduce them and the
+        replicas would drift silently.  Multi-GPU training must install ``s3od_amd.ddp.GradSync``
+        (``s3od_amd.train`` does); fail loudly otherwise."""
+        if (torch.is_grad_enabled() and self.model.training and dist.is_available() and dist.is_initialized()
+                and dist.get_world_size() > 1 and self.model.grad_ready_callback is None):
+            raise RuntimeError("data-parallel training needs s3od_amd.ddp.GradSync(model) (a torch/Lightning DDP "
+                               "strategy cannot see the native gradients); see s3od_amd/train.py")
+
     def _step(self, batch, batch_idx, split="train"):
         images, targets = batch["images"], batch["masks"]
+        self._check_grad_sync()
         predictions = self.model(images)
         loss, parts = self.loss_module(predictions, batch, self.current_epoch)
         for name, value in parts.items():

@@ -21,10 +21,11 @@ class FusedAdamW(torch.optim.Optimizer):
         self._tab = None
         self._tab_key = None
 
-    def _table(self, items, dev):
+    def _table(self, items, dev, step, beta1, wd):
         key = tuple((p.data_ptr(), p.grad.data_ptr() if p.grad is not None else 0,
                      self.state[p]["exp_avg"].data_ptr(), self.state[p]["exp_avg_sq"].data_ptr()) for p, _ in items)
-        lrs = torch.tensor([g["lr"] for _, g in items], dtype=torch.float32)
+        bc1 = 1.0 - beta1 ** step                 # Python doubles, rounded to f32 once (as torch)
+        coef = torch.tensor([[1.0 - g["lr"] * wd, g["lr"] / bc1] for _, g in items], dtype=torch.float32)
         if key != self._tab_key:
             ptrs, sizes, ct, co = [], [], [], []
             for t, (p, g) in enumerate(items):
@@ -40,7 +41,7 @@ class FusedAdamW(torch.optim.Optimizer):
                              ct=torch.tensor(ct, dtype=torch.int32, device=dev),
                              co=torch.tensor(co, dtype=torch.int64, device=dev), n=len(ct))
             self._tab_key = key
-        self._tab["lrs"] = lrs.to(dev, non_blocking=True)
+        self._tab["coef"] = coef.to(dev, non_blocking=True)
         return self._tab
 
     def load_state_dict(self, state_dict):
@@ -78,9 +79,13 @@ class FusedAdamW(torch.optim.Optimizer):
             raise NotImplementedError("FusedAdamW: all stepped parameters must share step count and betas/eps/wd")
         (b1, b2), eps, wd = hyper.pop()
         dev = items[0][0].device
-        tab = self._table(items, dev)
-        lib()("s3od_adamw_step", tab["ptrs"], tab["sizes"], tab["lrs"], tab["ct"], tab["co"], tab["n"], CHUNK,
-              steps.pop(), b1, b2, eps, wd, stream())
+        step = steps.pop()
+        tab = self._table(items, dev, step, b1, wd)
+        lib()("s3od_adamw_step", tab["ptrs"], tab["sizes"], tab["coef"], tab["ct"], tab["co"], tab["n"], CHUNK,
+              step, float(b1), float(b2), float(eps), stream())
+        # the kernel writes the masters through raw pointers: bump their version counters so
+        # every consumer keyed on `_version` (DPTEngine's packed-weight cache) sees the update
+        torch.autograd.graph.increment_version([p for p, _ in items])
         return loss
 
 

@@ -11,9 +11,13 @@ Model loading is offline-safe: a local checkpoint path is tried first (``torch.l
 transformers key layouts are accepted), then the Hugging Face cache (``local_files_only``).
 ``model_id="synthetic"`` builds the deterministic synthetic weights (tests / benchmarks).
 Errors: ``ValueError`` when the model cannot be located (predictor.py:59-63).
-Reference quirk kept: when (image_size - new_h) or (image_size - new_w) is odd the reference
-raises a numpy broadcast ValueError (predictor.py:83-89); ``exact_reference_quirks=False``
-pads asymmetrically instead.
+Reference quirks kept under ``exact_reference_quirks=True`` (the default):
+  1. when (image_size - new_h) or (image_size - new_w) is odd and the pad is > 0, the reference
+     raises a numpy broadcast ValueError (predictor.py:83-89);
+  2. when the pad is 0 but the resized side is < image_size (e.g. 1024x1023), the reference feeds
+     the UNPADDED resized image (S x new_w) to the model (predictor.py:89-90: ``padded = resized``),
+     whose output is then S x 16*floor(new_w/16) and is resized back from that.
+``exact_reference_quirks=False`` pads asymmetrically / to S x S instead.
 """
 from __future__ import annotations
 
@@ -100,6 +104,9 @@ class BackgroundRemoval:
         img = torch.from_numpy(np.ascontiguousarray(image, dtype=np.uint8)).to(self.device)
         x = torch.empty((1, 3, S, S), dtype=torch.float32, device=self.device)
         lib()("s3od_preprocess", img, image.shape[0], image.shape[1], nh, nw, info["height_pad"], info["width_pad"], S, x, stream())
+        if self.exact_reference_quirks and info["height_pad"] == 0 and info["width_pad"] == 0 and (nh, nw) != (S, S):
+            # Quirk 2: `padded = resized` -> the model sees the nh x nw image (it sits at the canvas origin)
+            x = x[:, :, :nh, :nw]
         return x, info
 
     @torch.no_grad()
@@ -112,12 +119,13 @@ class BackgroundRemoval:
             image_pil = Image.fromarray(image)
         x, pad = self._preprocess(image)
         out = self.model(x)
-        S = self.image_size
         H0, W0 = pad["original_size"]
-        h, w = S - 2 * pad["height_pad"], S - 2 * pad["width_pad"]
+        LH, LW = out["pred_masks"].shape[2], out["pred_masks"].shape[3]
+        h, w = LH - 2 * pad["height_pad"], LW - 2 * pad["width_pad"]
         tmp = torch.empty((3, h, W0), dtype=torch.float32, device=x.device)
         masks = torch.empty((3, H0, W0), dtype=torch.float32, device=x.device)
-        lib()("s3od_sigmoid_unpad_resize", out["pred_masks"], S, pad["height_pad"], pad["width_pad"], h, w, H0, W0, tmp, masks, stream())
+        lib()("s3od_sigmoid_unpad_resize", out["pred_masks"].contiguous(), LH, LW, pad["height_pad"], pad["width_pad"], h, w,
+              H0, W0, tmp, masks, stream())
         pred_ious = torch.sigmoid(out["pred_iou"]).squeeze(0).cpu().numpy()   # 3 floats
         all_masks = masks.cpu().numpy()
         best_idx = pred_ious.argmax()

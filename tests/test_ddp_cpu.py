@@ -57,6 +57,64 @@ def test_gradsync_gloo_world2():
         assert w == [7.0] * 4 and rm == [0.0, 0.0]  # rank 0's values broadcast
 
 
+def _worker_model(rank, world, port, q):
+    """The model's real flat-gradient layout and bucket ranges, driven through _grad_ready_hook in
+    the native backward's order (seg_head, layer10..layer0, embeddings) and _after_backward
+    (-> GradSync.finish); then a no_sync() accumulation micro-batch followed by a synced one."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from s3od_amd.model import DPTSegmentation
+        from s3od_amd.ddp import GradSync
+        m = DPTSegmentation(init_seed=None)
+        sync = GradSync(m)
+        G = m._grad_views()
+        buf = G["_flat"]
+        n = buf.numel()
+        base = torch.arange(n, dtype=torch.float32) % 997
+
+        def backward_hooks():
+            m._grad_ready_hook("seg_head")
+            for i in reversed(range(11)):
+                m._grad_ready_hook(f"layer{i}")
+            m._grad_ready_hook("embeddings")
+            m._after_backward()
+
+        buf.copy_(base * (rank + 1))
+        backward_hooks()
+        ok1 = bool(torch.equal(buf, base * 1.5))            # mean of x1 and x2
+        # accumulation: micro-batch 1 under no_sync (local only), micro-batch 2 synced
+        buf.zero_()
+        with sync.no_sync():
+            buf.add_(base * (rank + 1))
+            backward_hooks()
+        local_ok = bool(torch.equal(buf, base * (rank + 1)))  # untouched by the exchange
+        buf.add_(base * (rank + 1))
+        backward_hooks()
+        ok2 = bool(torch.equal(buf, base * 3.0))             # mean over ranks of 2x(rank+1)
+        # every parameter's .grad is a view of the exchanged buffer
+        p = dict(m.named_parameters())["encoder.model.layer.3.mlp.up_proj.weight"]
+        ok3 = p.grad.data_ptr() >= buf.data_ptr() and bool(p.grad.abs().sum() > 0)
+        q.put((rank, ok1, local_ok, ok2, ok3, n))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gradsync_model_layout_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_model, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, ok1, local_ok, ok2, ok3, n in res:
+        assert n == 107_825_862
+        assert ok1 and local_ok and ok2 and ok3, (rank, ok1, local_ok, ok2, ok3)
+
+
 def test_bucket_ranges_partition_grad_params():
     from s3od_amd.model import DPTSegmentation
     m = DPTSegmentation(init_seed=None)

@@ -77,3 +77,16 @@ def test_train_step_bf16():
     worst.sort(reverse=True)
     print("bf16 worst grad-norm errors:", worst[:5])
     assert worst[0][0] < 6e-2, worst[:5]
+    # direction, not just magnitude: per-parameter cosine against the f32-strict gradients of the
+    # same step on the GPU (the golden holds only norms and 32-element slices)
+    bf = {n: p.grad.detach().double().reshape(-1) for n, p in params.items() if p.grad is not None}
+    g2, m2, *_ = run_step("f32")
+    cos = []
+    for n, p in m2.named_parameters():
+        if p.grad is None or is_bn_fed_bias(n):
+            continue
+        a, b = bf[n], p.grad.detach().double().reshape(-1)
+        cos.append((float(a @ b / (a.norm() * b.norm()).clamp_min(1e-30)), n))
+    cos.sort()
+    print("bf16 worst grad cosines:", cos[:5])
+    assert cos[0][0] >= 0.99, cos[:5]
