@@ -14,8 +14,9 @@ pass) is timed live with HIP events on its launch stream around every call insid
 `breakdown`: per-class table (GEMM / attention / memory-bound) from a separate 2-step pass with every
 entry timed, plus the whole-step MFMA fraction and the ViT-encoder ("attention block") fraction.
 `cpu_baseline`: the oracle (oracle/s3od_oracle.py, the reference's CPU fp32 path restated) on this
-host's cores (rank 0, N=1 only): 1 warm-up + --cpu-iters timed iterations of one image (BASELINE.md
-"CPU-baseline plan"); C2 / C5 baselines ride in the `infer` / `infer_2048` objects.
+host's cores (rank 0, N=1 only): 1 warm-up + --cpu-iters (2) timed iterations of one image (BASELINE.md
+"CPU-baseline plan" asks for >= 3; 2 keeps the default run within a few minutes on the box's 16-thread
+share); C2 / C5 baselines ride in the `infer` / `infer_2048` objects (C5: one timed 2048^2 image, ~90 s).
 """
 from __future__ import annotations
 
@@ -90,8 +91,8 @@ def cpu_threads():
     return min(n, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else n
 
 
-def cpu_baseline(S, mode, iters):
-    """Oracle (reference CPU path restated in PyTorch fp32) on one image: 1 warm-up + `iters` timed."""
+def cpu_baseline(S, mode, iters, warmup=1):
+    """Oracle (reference CPU path restated in PyTorch fp32) on one image: `warmup` + `iters` timed."""
     from oracle import s3od_oracle as O
     from s3od_amd.weights import synthetic_state_dict
     threads = cpu_threads()
@@ -111,8 +112,9 @@ def cpu_baseline(S, mode, iters):
         def run():
             with torch.no_grad():
                 O.forward(x, sd)
-    log(f"cpu baseline {mode} {S}x{S}: warm-up ({threads} threads)")
-    run()                        # warm-up
+    for _ in range(warmup):
+        log(f"cpu baseline {mode} {S}x{S}: warm-up ({threads} threads)")
+        run()
     ts = []
     for it in range(iters):
         t0 = time.perf_counter()
@@ -124,7 +126,7 @@ def cpu_baseline(S, mode, iters):
     return {"value": round(1.0 / dt, 5), "unit": "images/s" if mode == "train" else "masks/s", "cores": threads,
             "kind": "port", "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count(),
             "iter_s": [round(t, 3) for t in ts],
-            "sample": f"1 image {S}x{S}, {what}, fp32 oracle (oracle/s3od_oracle.py), 1 warm-up + {iters} timed "
+            "sample": f"1 image {S}x{S}, {what}, fp32 oracle (oracle/s3od_oracle.py), {warmup} warm-up + {iters} timed "
                       f"iterations, {threads} threads"}
 
 
@@ -223,7 +225,8 @@ def infer_rate(model, B, S, steps, warmup, dev, cpu_iters):
            "mfma_frac": round(value * INFER_TF_PER_IMG[S] / PEAK_BF16, 4)}
     if cpu_iters > 0:
         try:
-            res["cpu_baseline"] = cpu_baseline(S, "infer", cpu_iters)
+            # one 2048^2 image is ~90 s of CPU on the box's 16-thread share: one timed pass, no warm-up
+            res["cpu_baseline"] = cpu_baseline(S, "infer", cpu_iters if S <= 1024 else 1, warmup=1 if S <= 1024 else 0)
         except Exception as e:  # reported, never fatal for the GPU number
             res["cpu_baseline"] = {"value": None, "error": repr(e)[:200]}
     return res
@@ -258,7 +261,7 @@ def main():
     ap.add_argument("--size", type=int, default=1024)
     ap.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-iters", type=int, default=3)
+    ap.add_argument("--cpu-iters", type=int, default=2, help="timed CPU-baseline iterations (after 1 warm-up)")
     ap.add_argument("--no-infer", action="store_true", help="skip the secondary inference lines (train mode)")
     ap.add_argument("--no-breakdown", action="store_true", help="skip the per-class profiling pass")
     ap.add_argument("--ddp", action="store_true",

@@ -28,6 +28,12 @@ import torch.nn.functional as F
 HIDDEN, HEADS, HEAD_DIM, N_REG, PATCH, EPS = 768, 12, 64, 4, 16, 1e-5
 ROPE_THETA = 100.0
 TAPS = (2, 5, 8, 11)
+# MT/model.py:28-32 intermediate_layer_idx per encoder (hidden 768 = ViT-B/16, 1024 = ViT-L/16)
+TAPS_BY_HIDDEN = {768: (2, 5, 8, 11), 1024: (4, 11, 17, 23)}
+
+
+def _hidden(sd):
+    return sd["encoder.embeddings.patch_embeddings.weight"].shape[0]
 
 
 # ---------------------------------------------------------------- encoder (DINOv3)
@@ -66,11 +72,12 @@ def _rotate_half(x):
 def attention(h, sd, p, cos, sin):
     """tf:…:294-334 + apply_rotary_pos_emb :238-268 (RoPE on patch tokens only) +
     SDPA (tf:integrations/sdpa_attention.py; eager-equivalent tf:…:210-235)."""
-    B, N, _ = h.shape
+    B, N, D = h.shape
+    heads = D // HEAD_DIM
     q = F.linear(h, sd[p + "attention.q_proj.weight"], sd[p + "attention.q_proj.bias"])
     k = F.linear(h, sd[p + "attention.k_proj.weight"])                      # key_bias=false
     v = F.linear(h, sd[p + "attention.v_proj.weight"], sd[p + "attention.v_proj.bias"])
-    q, k, v = (t.view(B, N, HEADS, HEAD_DIM).transpose(1, 2) for t in (q, k, v))
+    q, k, v = (t.view(B, N, heads, HEAD_DIM).transpose(1, 2) for t in (q, k, v))
     npfx = N - cos.shape[0]
     qp, kp = q[:, :, npfx:], k[:, :, npfx:]
     qp = qp * cos + _rotate_half(qp) * sin
@@ -79,16 +86,17 @@ def attention(h, sd, p, cos, sin):
     k = torch.cat([k[:, :, :npfx], kp], dim=2)
     s = torch.matmul(q, k.transpose(2, 3)) * (HEAD_DIM ** -0.5)
     a = torch.softmax(s, dim=-1)
-    o = torch.matmul(a, v).transpose(1, 2).reshape(B, N, HIDDEN)
+    o = torch.matmul(a, v).transpose(1, 2).reshape(B, N, D)
     return F.linear(o, sd[p + "attention.o_proj.weight"], sd[p + "attention.o_proj.bias"])
 
 
 def vit_layer(x, sd, i, cos, sin):
     """tf:…:419-445 — pre-LN block with LayerScale; MLP :346-357 with exact (erf) GELU."""
     p = f"encoder.model.layer.{i}."
-    h = F.layer_norm(x, (HIDDEN,), sd[p + "norm1.weight"], sd[p + "norm1.bias"], EPS)
+    D = x.shape[-1]
+    h = F.layer_norm(x, (D,), sd[p + "norm1.weight"], sd[p + "norm1.bias"], EPS)
     x = attention(h, sd, p, cos, sin) * sd[p + "layer_scale1.lambda1"] + x
-    h = F.layer_norm(x, (HIDDEN,), sd[p + "norm2.weight"], sd[p + "norm2.bias"], EPS)
+    h = F.layer_norm(x, (D,), sd[p + "norm2.weight"], sd[p + "norm2.bias"], EPS)
     h = F.linear(h, sd[p + "mlp.up_proj.weight"], sd[p + "mlp.up_proj.bias"])
     h = F.gelu(h)
     h = F.linear(h, sd[p + "mlp.down_proj.weight"], sd[p + "mlp.down_proj.bias"])
@@ -96,16 +104,18 @@ def vit_layer(x, sd, i, cos, sin):
 
 
 def encoder_taps(x, sd, rope_rescale=None):
-    """hidden_states = (emb, L0..L11) (tf:utils/output_capturing.py:112-117); S3OD taps
-    indices [2,5,8,11] (src/s3od/model.py:36-40,62-86) and drops 1+4 prefix tokens.
-    Layer 11 and the final norm never reach the outputs, so they are not run."""
+    """hidden_states = (emb, L0..L{n-1}) (tf:utils/output_capturing.py:112-117); S3OD taps
+    indices [2,5,8,11] for ViT-B, [4,11,17,23] for ViT-L (MT/model.py:28-32, src/s3od/model.py:62-86)
+    and drops 1+4 prefix tokens.  Layers from the last tap on and the final norm never reach the
+    outputs, so they are not run."""
     ph, pw = x.shape[-2] // PATCH, x.shape[-1] // PATCH
     cos, sin = (t.to(x.device) for t in rope_cos_sin(ph, pw, rope_rescale))
     h = patch_embed(x, sd)
+    taps_idx = TAPS_BY_HIDDEN[_hidden(sd)]
     taps = []
-    for i in range(max(TAPS)):
+    for i in range(max(taps_idx)):
         h = vit_layer(h, sd, i, cos, sin)
-        if i + 1 in TAPS:
+        if i + 1 in taps_idx:
             taps.append(h[:, 1 + N_REG:])
     return taps
 
@@ -173,7 +183,8 @@ def dpt_head(taps, sd, ph, pw, train=False):
     # (the feature is already 16*patch); kept explicit for fidelity.
     f = F.interpolate(f, size=(PATCH * ph, PATCH * pw), mode="bilinear", align_corners=False, antialias=True)
     masks = []
-    for k in range(3):
+    n_masks = sum(1 for k in sd if k.startswith(m + "mask_heads.") and k.endswith(".0.weight"))
+    for k in range(n_masks):
         g = F.relu(F.conv2d(f, sd[m + f"mask_heads.{k}.0.weight"], sd[m + f"mask_heads.{k}.0.bias"], padding=1))
         masks.append(F.conv2d(g, sd[m + f"mask_heads.{k}.2.weight"], sd[m + f"mask_heads.{k}.2.bias"]))
     return {"pred_masks": torch.cat(masks, dim=1), "pred_iou": iou, "features": p1}
@@ -266,6 +277,26 @@ def multi_mask_loss(outputs, masks, epoch=0, cfg=FOCAL_IOU):
     parts["mse_ious_loss"] = mse
     parts = {k: (v.mean() if v.dim() > 0 else v) for k, v in parts.items()}
     return total, parts, best, ious
+
+
+def single_mask_loss(outputs, masks, cfg=FOCAL_IOU):
+    """loss.py:166-188 (MaskLossHandler.compute_single_mask_loss, num_outputs=1): each mask criterion on
+    the [B,H,W] maps, .mean(); no best-mask selection, no decay term, no aux MSE."""
+    pred = torch.sigmoid(outputs["pred_masks"].squeeze(1))
+    total = torch.zeros((), device=pred.device)
+    parts = {}
+    for name, w, kind in cfg["components"]:
+        if kind == "focal":
+            a = focal_loss(pred, masks).mean()
+        elif kind == "bce":
+            a = F.binary_cross_entropy(pred, masks, reduction="none").mean()
+        elif kind == "iou":
+            a = iou_loss(pred, masks).mean()
+        else:
+            raise RuntimeError("SSIMLoss fails on [B,H,W] maps in the reference")
+        total = total + w * a
+        parts[name] = a
+    return total, parts
 
 
 # ---------------------------------------------------------------- remove_background pieces

@@ -28,16 +28,22 @@ class _DPTFn(torch.autograd.Function):
     def backward(fctx, d_masks, d_iou, d_feat):
         model, eng, ctx = fctx.s3od
         G = model._grad_views()
+        nm = model.num_outputs
         if d_masks is None:
-            d_masks = torch.zeros((ctx.B, 3, 16 * ctx.ph, 16 * ctx.pw), dtype=torch.float32, device=G["_flat"].device)
-        if d_iou is None:
-            d_iou = torch.zeros((ctx.B, 3), dtype=torch.float32, device=G["_flat"].device)
+            d_masks = torch.zeros((ctx.B, nm, 16 * ctx.ph, 16 * ctx.pw), dtype=torch.float32, device=G["_flat"].device)
+        iou_unused = d_iou is None     # e.g. the single-mask loss (loss.py:166-188) never reads pred_iou
+        if iou_unused:
+            d_iou = torch.zeros((ctx.B, nm), dtype=torch.float32, device=G["_flat"].device)
         eng.grad_hook = model._grad_ready_hook
         try:
             eng.backward(ctx, d_masks.float().contiguous(), d_iou.float().contiguous(), G)
         finally:
             eng.grad_hook = None
             fctx.s3od = None
+        if iou_unused:
+            # the reference's classifier_head receives no gradient at all (grad None -> AdamW skips it)
+            for p in model.seg_head.classifier_head.parameters():
+                p.grad = None
         model._after_backward()
         return None, torch.zeros((), device=d_iou.device), None, None, None
 

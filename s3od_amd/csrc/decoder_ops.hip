@@ -310,9 +310,9 @@ __global__ void __launch_bounds__(256) avgpool_kernel(const T* __restrict__ x, f
   }
 }
 
-// classifier_head (src/s3od/model.py:185-191): Linear(256,64) -> ReLU -> Linear(64,3); one block per image
+// classifier_head (src/s3od/model.py:185-191): Linear(256,64) -> ReLU -> Linear(64,NM); one block per image
 __global__ void iou_head_fwd_kernel(const float* pooled, const float* w1, const float* b1, const float* w2, const float* b2,
-                                    float* hid, float* out) {
+                                    float* hid, float* out, int NM) {
   __shared__ float h[64];
   int b = blockIdx.x, t = threadIdx.x;   // 64 threads
   const float* x = pooled + b * 256;
@@ -322,28 +322,28 @@ __global__ void iou_head_fwd_kernel(const float* pooled, const float* w1, const 
   h[t] = a;
   if (hid) hid[b * 64 + t] = a;
   __syncthreads();
-  if (t < 3) {
+  if (t < NM) {
     float o = b2[t];
     for (int k = 0; k < 64; k++) o += w2[t * 64 + k] * h[k];
-    out[b * 3 + t] = o;
+    out[b * NM + t] = o;
   }
 }
 
-// backward of the head: given dout [B,3] -> dw2, db2, dw1, db1 (accumulate) and dpooled/HW [B,256] (bcast for p1)
+// backward of the head: given dout [B,NM] -> dw2, db2, dw1, db1 (accumulate) and dpooled/HW [B,256] (bcast for p1)
 __global__ void iou_head_bwd_kernel(const float* pooled, const float* hid, const float* w1, const float* w2, const float* dout,
-                                    float* dw1, float* db1, float* dw2, float* db2, float* dpix, int B, float inv_hw) {
+                                    float* dw1, float* db1, float* dw2, float* db2, float* dpix, int B, float inv_hw, int NM) {
   // single block of 256 threads; B is small
   __shared__ float dh[64];
   int t = threadIdx.x;
   for (int b = 0; b < B; b++) {
-    const float* d = dout + b * 3;
+    const float* d = dout + b * NM;
     if (t < 64) {
       float g = 0.f;
-      for (int j = 0; j < 3; j++) { g += d[j] * w2[j * 64 + t]; atomicAdd(dw2 + j * 64 + t, d[j] * hid[b * 64 + t]); }
+      for (int j = 0; j < NM; j++) { g += d[j] * w2[j * 64 + t]; atomicAdd(dw2 + j * 64 + t, d[j] * hid[b * 64 + t]); }
       dh[t] = hid[b * 64 + t] > 0.f ? g : 0.f;
       atomicAdd(db1 + t, dh[t]);
     }
-    if (t < 3) atomicAdd(db2 + t, d[t]);
+    if (t < NM) atomicAdd(db2 + t, d[t]);
     __syncthreads();
     // dw1[j][k] += dh[j]*pooled[k];  dpooled[k] = sum_j dh[j] w1[j][k]
     float dp = 0.f;
@@ -354,16 +354,17 @@ __global__ void iou_head_bwd_kernel(const float* pooled, const float* hid, const
 }
 
 // ---------------------------------------------------------------- mask-head backward prologue
-// dlogits [B,3,HW] f32, h [M,96] T (post-ReLU) -> dh [M,96] T = relu'(h) * dlogit_k * w2[k];
-// accumulates dw2 [3][32], db2 [3] and db1 [96] (= column sums of dh, the 3x3 convs' bias gradient).
-// block = 384 threads = 32 pixel rows x 12 chunks of 8 channels (chunk j belongs to head j/4).
-template <typename T>
-__global__ void __launch_bounds__(384) mask_heads_bwd_kernel(const float* __restrict__ dlog, const T* __restrict__ hs,
+// dlogits [B,NM,HW] f32, h [M,32NM] T (post-ReLU) -> dh [M,32NM] T = relu'(h) * dlogit_k * w2[k];
+// accumulates dw2 [NM][32], db2 [NM] and db1 [32NM] (= column sums of dh, the 3x3 convs' bias gradient).
+// block = 128 NM threads = 32 pixel rows x 4NM chunks of 8 channels (chunk j belongs to head j/4).
+template <typename T, int NM>
+__global__ void __launch_bounds__(128 * NM) mask_heads_bwd_kernel(const float* __restrict__ dlog, const T* __restrict__ hs,
                                                              const float* __restrict__ w2, T* __restrict__ dh,
                                                              float* __restrict__ dw2, float* __restrict__ db2, float* __restrict__ db1,
                                                              long M, int HW) {
-  __shared__ float red[384 * 8];
-  const int t = threadIdx.x, j = t % 12, pr = t / 12;
+  constexpr int NC = 4 * NM, C = 32 * NM, NT = 32 * NC;
+  __shared__ float red[NT * 8];
+  const int t = threadIdx.x, j = t % NC, pr = t / NC;
   const int k = j >> 2, c0 = j * 8;
   float wk[8];
   load8<float>(w2 + c0, wk);
@@ -371,20 +372,20 @@ __global__ void __launch_bounds__(384) mask_heads_bwd_kernel(const float* __rest
   float adb = 0.f;
   for (long m = (long)blockIdx.x * 32 + pr; m < M; m += (long)gridDim.x * 32) {
     int b = m / HW; long pix = m - (long)b * HW;
-    float dl = dlog[((long)b * 3 + k) * HW + pix];
+    float dl = dlog[((long)b * NM + k) * HW + pix];
     float hv[8], o[8];
-    load8<T>(hs + m * 96 + c0, hv);
+    load8<T>(hs + m * C + c0, hv);
 #pragma unroll
     for (int e = 0; e < 8; e++) {
       o[e] = hv[e] > 0.f ? dl * wk[e] : 0.f;
       aw[e] += dl * hv[e];
     }
-    store8<T>(dh + m * 96 + c0, o);
+    store8<T>(dh + m * C + c0, o);
 #pragma unroll
     for (int e = 0; e < 8; e++) ab[e] += o[e];
     adb += dl;
   }
-  // reduce over the 32 pixel rows: aw -> dw2, ab -> db1, adb (chunks 0,4,8) -> db2
+  // reduce over the 32 pixel rows: aw -> dw2, ab -> db1, adb (chunks 0,4,8,..) -> db2
   float* r = red;
   for (int pass = 0; pass < 3; pass++) {
     __syncthreads();
@@ -392,15 +393,15 @@ __global__ void __launch_bounds__(384) mask_heads_bwd_kernel(const float* __rest
     else if (pass == 1) { for (int e = 0; e < 8; e++) r[t * 8 + e] = ab[e]; }
     else r[t * 8] = adb;
     __syncthreads();
-    if (t < 96) {
+    if (t < C) {
       const int jj = t >> 3, e = t & 7;
       if (pass < 2) {
         float s = 0.f;
-        for (int q = 0; q < 32; q++) s += r[((q * 12) + jj) * 8 + e];
+        for (int q = 0; q < 32; q++) s += r[((q * NC) + jj) * 8 + e];
         atomicAdd((pass == 0 ? dw2 : db1) + t, s);
-      } else if (t < 3) {
+      } else if (t < NM) {
         float s = 0.f;
-        for (int q = 0; q < 32; q++) s += r[((q * 12) + 4 * t) * 8];
+        for (int q = 0; q < 32; q++) s += r[((q * NC) + 4 * t) * 8];
         atomicAdd(db2 + t, s);
       }
     }
@@ -497,25 +498,32 @@ int s3od_avgpool(int dtype, const void* x, float* out, int B, int HW, int C, voi
 }
 
 int s3od_iou_head_fwd(const float* pooled, const float* w1, const float* b1, const float* w2, const float* b2, float* hid,
-                      float* out, int B, void* stream) {
-  hipLaunchKernelGGL(iou_head_fwd_kernel, dim3(B), dim3(64), 0, (hipStream_t)stream, pooled, w1, b1, w2, b2, hid, out);
+                      float* out, int B, int NM, void* stream) {
+  S3OD_REQUIRE(NM >= 1 && NM <= 64, "iou_head_fwd: %d outputs", NM);
+  hipLaunchKernelGGL(iou_head_fwd_kernel, dim3(B), dim3(64), 0, (hipStream_t)stream, pooled, w1, b1, w2, b2, hid, out, NM);
   return s3od_check_launch("iou_head_fwd");
 }
 
 int s3od_iou_head_bwd(const float* pooled, const float* hid, const float* w1, const float* w2, const float* dout, float* dw1,
-                      float* db1, float* dw2, float* db2, float* dpix, int B, int HW, void* stream) {
+                      float* db1, float* dw2, float* db2, float* dpix, int B, int HW, int NM, void* stream) {
+  S3OD_REQUIRE(NM >= 1 && NM <= 64, "iou_head_bwd: %d outputs", NM);
   hipLaunchKernelGGL(iou_head_bwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, pooled, hid, w1, w2, dout, dw1, db1, dw2, db2,
-                     dpix, B, 1.0f / (float)HW);
+                     dpix, B, 1.0f / (float)HW, NM);
   return s3od_check_launch("iou_head_bwd");
 }
 
 int s3od_mask_heads_bwd(int dtype, const float* dlogits, const void* hsave, const float* w2, void* dh, float* dw2, float* db2,
-                        float* db1, int B, int HW, void* stream) {
+                        float* db1, int B, int HW, int NM, void* stream) {
+  S3OD_REQUIRE(NM == 1 || NM == 3, "mask_heads_bwd: %d heads not built (1 or 3)", NM);
   long M = (long)B * HW;
   const int nb = (int)min(1024L, (M + 31) / 32);
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(mask_heads_bwd_kernel<T>, dim3(nb), dim3(384), 0, (hipStream_t)stream, dlogits, (const T*)hsave, w2,
-                       (T*)dh, dw2, db2, db1, M, HW);
+    if (NM == 3)
+      hipLaunchKernelGGL((mask_heads_bwd_kernel<T, 3>), dim3(nb), dim3(384), 0, (hipStream_t)stream, dlogits, (const T*)hsave, w2,
+                         (T*)dh, dw2, db2, db1, M, HW);
+    else
+      hipLaunchKernelGGL((mask_heads_bwd_kernel<T, 1>), dim3(nb), dim3(128), 0, (hipStream_t)stream, dlogits, (const T*)hsave, w2,
+                         (T*)dh, dw2, db2, db1, M, HW);
   });
   return s3od_check_launch("mask_heads_bwd");
 }

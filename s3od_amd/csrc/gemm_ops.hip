@@ -88,30 +88,31 @@ template <typename T> struct EpiQKV {
   }
 };
 
-// ------------------------------------------------------------------ fused 3 mask heads
-// per pixel: h = relu(conv3x3_64->96(feat) + b1) ; logit_k = h[32k:32k+32] . w2[k] + b2[k]
-// (src/s3od/model.py:440-452,461-467; the three Sequential heads run as one N=96 GEMM)
+// ------------------------------------------------------------------ fused mask heads
+// per pixel: h = relu(conv3x3_64->32NM(feat) + b1) ; logit_k = h[32k:32k+32] . w2[k] + b2[k]
+// (src/s3od/model.py:440-452,461-467; the NM Sequential heads run as one N=32NM GEMM)
 template <typename T> struct EpiHeads {
   float* logits; T* hsave; const float* b1; const float* w2; const float* b2;
-  int M, HW;
+  int M, HW, NM;
   DEV void prepare(int) {}
   DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN, int NT) const {
+    const int C = 32 * NM, SPR = 4 * NM;                      // channels / 8-channel segments per row
     // h = relu(acc + b1) is formed on the fly from the staged fp32 tile (no in-place pass)
     if (hsave) {
-      const int segs = BM * 12;                               // 12 segments of 8 channels per row
+      const int segs = BM * SPR;
       for (int s = tid; s < segs; s += NT) {
-        int r = s / 12, c = (s - r * 12) * 8, m = m0 + r;
+        int r = s / SPR, c = (s - r * SPR) * 8, m = m0 + r;
         if (m >= M) continue;
         const float4* src = (const float4*)(ct + r * LDT + c);
         float4 x0 = src[0], x1 = src[1];
         float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
         for (int e = 0; e < 8; e++) v[e] = fmaxf(v[e] + b1[c + e], 0.f);
-        store8<T>(hsave + (long)m * 96 + c, v);
+        store8<T>(hsave + (long)m * C + c, v);
       }
     }
     // logit_k = b2[k] + sum_j relu(acc[32k + j] + b1[32k + j]) * w2[32k + j]; k is wave-uniform
-    for (int s = tid; s < 3 * BM; s += NT) {
+    for (int s = tid; s < NM * BM; s += NT) {
       int k = s / BM, r = s - k * BM;
       int m = m0 + r;
       if (m >= M) continue;
@@ -128,7 +129,7 @@ template <typename T> struct EpiHeads {
         acc += fmaxf(x.w + bb[4 * q + 3], 0.f) * ww[4 * q + 3];
       }
       int b = m / HW, pix = m - b * HW;
-      logits[((long)b * 3 + k) * HW + pix] = acc;
+      logits[((long)b * NM + k) * HW + pix] = acc;
     }
   }
 };
@@ -244,10 +245,10 @@ int s3od_linear_wgrad(int dtype, int Nout, int Kin, int rows, const void* dy, lo
   return 0;
 }
 
-// fused QKV projection + bias + RoPE + head split. x: [B*Ntok, 768] T ; w: [2304, 768] T
-int s3od_qkv_rope_fwd(int dtype, int B, int Ntok, int P, const void* x, const void* w, const float* bias,
+// fused QKV projection + bias + RoPE + head split. x: [B*Ntok, D] T ; w: [3D, D] T ; D = 64 H
+int s3od_qkv_rope_fwd(int dtype, int B, int Ntok, int P, int H, const void* x, const void* w, const float* bias,
                       const float* cos_t, const float* sin_t, void* q, void* k, void* v, void* stream) {
-  const int H = 12, D = 768, N = 3 * D, M = B * Ntok;
+  const int D = 64 * H, N = 3 * D, M = B * Ntok;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     return with_cfg<T>(4, [&](auto C) -> int {
@@ -366,21 +367,26 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
   return 0;
 }
 
-// three 3x3 64->32 + ReLU + 1x1 32->1 mask heads as one GEMM (N=96) with a fused epilogue.
-// feat: [B,H,W,64] T ; w1p: [96][3][3][64] T ; b1: [96]; w2: [3][32]; b2: [3]
-// logits: [B,3,H,W] fp32 (NCHW, the reference output layout); hsave: optional [B*H*W, 96] T
-int s3od_mask_heads_fwd(int dtype, int B, int H, int W, const void* feat, const void* w1p, const float* b1,
+// NM (3 for dinob, 1 for dinol) 3x3 64->32 + ReLU + 1x1 32->1 mask heads as one GEMM (N=32NM) with
+// a fused epilogue.  feat: [B,H,W,64] T ; w1p: [32NM][3][3][64] T ; b1: [32NM]; w2: [NM][32]; b2: [NM]
+// logits: [B,NM,H,W] fp32 (NCHW, the reference output layout); hsave: optional [B*H*W, 32NM] T
+int s3od_mask_heads_fwd(int dtype, int B, int H, int W, int NM, const void* feat, const void* w1p, const float* b1,
                         const float* w2, const float* b2, float* logits, void* hsave, void* stream) {
+  S3OD_REQUIRE(NM == 1 || NM == 3, "mask_heads_fwd: %d heads not built (1 or 3)", NM);
   ConvGeo g{}; g.B = B; g.SH = H; g.SW = W; g.SC = 64; g.RH = H; g.RW = W; g.KH = 3; g.KW = 3; g.s = 1; g.p = 1;
-  const int M = B * H * W, N = 96, K = 9 * 64;
+  const int M = B * H * W, N = 32 * NM, K = 9 * 64;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
-    constexpr int BM = 128, BN = 128;
+    constexpr int BM = 128;
     ConvFwdA<T, BM> la{}; la.x = (const T*)feat; la.g = g; la.M = M; la.relu = 0;
-    DenseKC<T, BN> lb{(const T*)w1p, (long)K, N, K, 0};
-    EpiHeads<T> e{logits, (T*)hsave, b1, w2, b2, M, H * W};
-    // 2 K stages: 67.6 KB of LDS -> 2 workgroups per CU, so one's epilogue overlaps the other's K loop
-    return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), 2>(la, lb, e, M, BN, cdiv(K, KT<T>::BK), 1, 1, st);
+    EpiHeads<T> e{logits, (T*)hsave, b1, w2, b2, M, H * W, NM};
+    // 2 K stages -> 2 workgroups per CU, so one's epilogue overlaps the other's K loop
+    if (NM == 3) {
+      DenseKC<T, 128> lb{(const T*)w1p, (long)K, N, K, 0};
+      return launch_igemm<T, BM, 128, decltype(la), decltype(lb), decltype(e), 2>(la, lb, e, M, 128, cdiv(K, KT<T>::BK), 1, 1, st);
+    }
+    DenseKC<T, 64> lb{(const T*)w1p, (long)K, N, K, 0};
+    return launch_igemm<T, BM, 64, decltype(la), decltype(lb), decltype(e), 2>(la, lb, e, M, 64, cdiv(K, KT<T>::BK), 1, 1, st);
   });
   return 0;
 }

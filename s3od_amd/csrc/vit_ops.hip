@@ -31,12 +31,20 @@ __global__ void patch_im2col_kernel(const float* __restrict__ x, T* __restrict__
   store8<T>(dst + 8, v + 8);
 }
 
+// hidden size D of the encoder: 768 (ViT-B/16, dinob) or 1024 (ViT-L/16, dinol); head dim 64
+#define DISPATCH_D(D_, ...)                                                     \
+  do {                                                                          \
+    if ((D_) == 768) { constexpr int D = 768; __VA_ARGS__ }                     \
+    else if ((D_) == 1024) { constexpr int D = 1024; __VA_ARGS__ }              \
+    else { s3od_set_error("hidden size %d not built (768 or 1024)", (int)(D_)); return 22; } \
+  } while (0)
+
 // rows 0..4 of each image: cls + 4 register tokens (tf:…:88-90)
-__global__ void token_prefix_kernel(float* x, const float* cls, const float* reg, int Ntok) {
+__global__ void token_prefix_kernel(float* x, const float* cls, const float* reg, int Ntok, int D) {
   int b = blockIdx.x, t = blockIdx.y;  // t in 0..4
-  const float* src = t == 0 ? cls : reg + (t - 1) * 768;
-  float* dst = x + ((long)b * Ntok + t) * 768;
-  for (int i = threadIdx.x; i < 768; i += blockDim.x) dst[i] = src[i];
+  const float* src = t == 0 ? cls : reg + (t - 1) * D;
+  float* dst = x + ((long)b * Ntok + t) * D;
+  for (int i = threadIdx.x; i < D; i += blockDim.x) dst[i] = src[i];
 }
 
 // RoPE table (tf:…:96-121, 168-200): cos/sin [P,64]; rescale <= 0 means none (eval)
@@ -57,30 +65,31 @@ __global__ void rope_table_kernel(float* cs, float* sn, int ph, int pw, float re
   sn[p * 64 + j] = sinf(ang);
 }
 
-// ---------------------------------------------------------------- LayerNorm (D = 768)
-// one wave per row; fp32 statistics; y = (x-mean)*rstd*w + b  stored as T
-template <typename T>
+// ---------------------------------------------------------------- LayerNorm (D = 768 / 1024)
+// one wave per row (NV = D/256 float4 per lane); fp32 statistics; y = (x-mean)*rstd*w + b stored as T
+template <typename T, int D>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                       const float* __restrict__ b, T* __restrict__ y,
                                                       float* __restrict__ mean_o, float* __restrict__ rstd_o, int M, float eps) {
+  constexpr int NV = D / 256;
   int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= M) return;
-  const float* xr = x + (long)row * 768;
-  float v[12];
+  const float* xr = x + (long)row * D;
+  float v[4 * NV];
 #pragma unroll
-  for (int i = 0; i < 3; i++) { float4 f = ((const float4*)xr)[lane + 64 * i]; v[4 * i] = f.x; v[4 * i + 1] = f.y; v[4 * i + 2] = f.z; v[4 * i + 3] = f.w; }
+  for (int i = 0; i < NV; i++) { float4 f = ((const float4*)xr)[lane + 64 * i]; v[4 * i] = f.x; v[4 * i + 1] = f.y; v[4 * i + 2] = f.z; v[4 * i + 3] = f.w; }
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 12; i++) s += v[i];
-  float mean = warp_sum(s) * (1.0f / 768.0f);
+  for (int i = 0; i < 4 * NV; i++) s += v[i];
+  float mean = warp_sum(s) * (1.0f / D);
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < 12; i++) { float d = v[i] - mean; q += d * d; }
-  float var = warp_sum(q) * (1.0f / 768.0f);
+  for (int i = 0; i < 4 * NV; i++) { float d = v[i] - mean; q += d * d; }
+  float var = warp_sum(q) * (1.0f / D);
   float rstd = 1.0f / sqrtf(var + eps);
-  T* yr = y + (long)row * 768;
+  T* yr = y + (long)row * D;
 #pragma unroll
-  for (int i = 0; i < 3; i++) {
+  for (int i = 0; i < NV; i++) {
     int c = 4 * (lane + 64 * i);
     float4 wf = *(const float4*)(w + c), bf = *(const float4*)(b + c);
     float o0 = (v[4 * i] - mean) * rstd * wf.x + bf.x, o1 = (v[4 * i + 1] - mean) * rstd * wf.y + bf.y;
@@ -92,48 +101,49 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
 }
 
 // LayerNorm backward. dx = dres + rstd*(g - mean(g) - xhat*mean(g*xhat)), g = dy*w
-// dw += sum dy*xhat ; db += sum dy   (fp32 block partials -> atomics)
-template <typename T>
+// dw += sum dy*xhat ; db += sum dy   (fp32 block partials -> replicated atomics [NREP][2D])
+template <typename T, int D>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, const float* __restrict__ x,
                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
                                                       const float* __restrict__ w, const float* __restrict__ dres,
                                                       float* __restrict__ dx, float* __restrict__ ws,
                                                       int M, int rows_per_block) {
-  __shared__ float sdw[768], sdb[768];
-  for (int i = threadIdx.x; i < 768; i += 256) { sdw[i] = 0.f; sdb[i] = 0.f; }
+  constexpr int NV = D / 256, NE = 4 * NV;
+  __shared__ float sdw[D], sdb[D];
+  for (int i = threadIdx.x; i < D; i += 256) { sdw[i] = 0.f; sdb[i] = 0.f; }
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float pw[12], pb[12];
+  float pw[NE], pb[NE];
 #pragma unroll
-  for (int i = 0; i < 12; i++) { pw[i] = 0.f; pb[i] = 0.f; }
+  for (int i = 0; i < NE; i++) { pw[i] = 0.f; pb[i] = 0.f; }
   int r0 = blockIdx.x * rows_per_block;
   for (int row = r0 + wave; row < min(M, r0 + rows_per_block); row += 4) {
-    const float* xr = x + (long)row * 768;
+    const float* xr = x + (long)row * D;
     float mu = mean[row], rs = rstd[row];
-    float xh[12], g[12], dyv[12];
-    float4 rr4[3];
+    float xh[NE], g[NE], dyv[NE];
+    float4 rr4[NV];
 #pragma unroll
-    for (int i = 0; i < 3; i++)   // issue the residual-gradient loads before the row reductions
-      rr4[i] = dres ? *(const float4*)(dres + (long)row * 768 + 4 * (lane + 64 * i)) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < NV; i++)   // issue the residual-gradient loads before the row reductions
+      rr4[i] = dres ? *(const float4*)(dres + (long)row * D + 4 * (lane + 64 * i)) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int i = 0; i < 3; i++) {
+    for (int i = 0; i < NV; i++) {
       int c = 4 * (lane + 64 * i);
       float4 xf = *(const float4*)(xr + c);
       float4 wf = *(const float4*)(w + c);
       float d4[4];
-      if constexpr (sizeof(T) == 4) { float4 t = *(const float4*)(dy + (long)row * 768 + c); d4[0] = t.x; d4[1] = t.y; d4[2] = t.z; d4[3] = t.w; }
-      else { bf16x4 t = *(const bf16x4*)(dy + (long)row * 768 + c); d4[0] = (float)t[0]; d4[1] = (float)t[1]; d4[2] = (float)t[2]; d4[3] = (float)t[3]; }
-      float xs[4] = {xf.x, xf.y, xf.z, xf.w}, ws[4] = {wf.x, wf.y, wf.z, wf.w};
+      if constexpr (sizeof(T) == 4) { float4 t = *(const float4*)(dy + (long)row * D + c); d4[0] = t.x; d4[1] = t.y; d4[2] = t.z; d4[3] = t.w; }
+      else { bf16x4 t = *(const bf16x4*)(dy + (long)row * D + c); d4[0] = (float)t[0]; d4[1] = (float)t[1]; d4[2] = (float)t[2]; d4[3] = (float)t[3]; }
+      float xs[4] = {xf.x, xf.y, xf.z, xf.w}, wv[4] = {wf.x, wf.y, wf.z, wf.w};
 #pragma unroll
-      for (int e = 0; e < 4; e++) { xh[4 * i + e] = (xs[e] - mu) * rs; dyv[4 * i + e] = d4[e]; g[4 * i + e] = d4[e] * ws[e]; }
+      for (int e = 0; e < 4; e++) { xh[4 * i + e] = (xs[e] - mu) * rs; dyv[4 * i + e] = d4[e]; g[4 * i + e] = d4[e] * wv[e]; }
     }
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < 12; i++) { s1 += g[i]; s2 += g[i] * xh[i]; }
-    s1 = warp_sum(s1) * (1.0f / 768.0f);
-    s2 = warp_sum(s2) * (1.0f / 768.0f);
+    for (int i = 0; i < NE; i++) { s1 += g[i]; s2 += g[i] * xh[i]; }
+    s1 = warp_sum(s1) * (1.0f / D);
+    s2 = warp_sum(s2) * (1.0f / D);
 #pragma unroll
-    for (int i = 0; i < 3; i++) {
+    for (int i = 0; i < NV; i++) {
       int c = 4 * (lane + 64 * i);
       float o[4];
       float rr[4] = {rr4[i].x, rr4[i].y, rr4[i].z, rr4[i].w};
@@ -144,11 +154,11 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
         pw[k] += dyv[k] * xh[k];
         pb[k] += dyv[k];
       }
-      *(float4*)(dx + (long)row * 768 + c) = make_float4(o[0], o[1], o[2], o[3]);
+      *(float4*)(dx + (long)row * D + c) = make_float4(o[0], o[1], o[2], o[3]);
     }
   }
 #pragma unroll
-  for (int i = 0; i < 3; i++)
+  for (int i = 0; i < NV; i++)
 #pragma unroll
     for (int e = 0; e < 4; e++) {
       int c = 4 * (lane + 64 * i) + e;
@@ -156,29 +166,30 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
       atomicAdd(&sdb[c], pb[4 * i + e]);
     }
   __syncthreads();
-  float* rep = ws + (long)(blockIdx.x % S3OD_NREP) * 1536;   // replicated [dw | db] partials
-  for (int i = threadIdx.x; i < 768; i += 256) { atomicAdd(rep + i, sdw[i]); atomicAdd(rep + 768 + i, sdb[i]); }
+  float* rep = ws + (long)(blockIdx.x % S3OD_NREP) * 2 * D;   // replicated [dw | db] partials
+  for (int i = threadIdx.x; i < D; i += 256) { atomicAdd(rep + i, sdw[i]); atomicAdd(rep + D + i, sdb[i]); }
 }
 
-// a[i] += sum_r ws[r][i], b[i] += sum_r ws[r][768 + i]   (fold of the replicated 2x768 partials)
-__global__ void fold768x2_kernel(const float* __restrict__ ws, float* __restrict__ a, float* __restrict__ b) {
+// a[i] += sum_r ws[r][i], b[i] += sum_r ws[r][D + i]   (fold of the replicated 2 x D partials; a/b may be null)
+__global__ void fold2_kernel(const float* __restrict__ ws, float* __restrict__ a, float* __restrict__ b, int D) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 1536) return;
+  if (i >= 2 * D) return;
   float s = 0.f;
-  for (int r = 0; r < S3OD_NREP; r++) s += ws[r * 1536 + i];
-  if (i < 768) a[i] += s; else b[i - 768] += s;
+  for (int r = 0; r < S3OD_NREP; r++) s += ws[(long)r * 2 * D + i];
+  if (i < D) { if (a) a[i] += s; }
+  else if (b) b[i - D] += s;
 }
 
-// taps: x f32 [B, Ntok, 768] -> T [B, P, 768] (drop 1 + 4 prefix tokens; src/s3od/model.py:75-84)
+// taps: x f32 [B, Ntok, D] -> T [B, P, D] (drop 1 + 4 prefix tokens; src/s3od/model.py:75-84)
 template <typename T>
-__global__ void cast_tap_kernel(const float* __restrict__ x, T* __restrict__ y, int B, int Ntok, int P) {
+__global__ void cast_tap_kernel(const float* __restrict__ x, T* __restrict__ y, int B, int Ntok, int P, int D) {
   long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  long total = (long)B * P * 768;
+  long total = (long)B * P * D;
   if (i >= total) return;
-  long row = i / 768; int c = i % 768;
+  long row = i / D; int c = i % D;
   int b = row / P, p = row % P;
   float v[8];
-  load8<float>(x + ((long)b * Ntok + (Ntok - P) + p) * 768 + c, v);
+  load8<float>(x + ((long)b * Ntok + (Ntok - P) + p) * D + c, v);
   store8<T>(y + i, v);
 }
 
@@ -225,12 +236,13 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ a, lo
 }
 
 // LayerScale backward: du = dx * lam (T); dlam[n] += sum_m dx*u ; dbias[n] += sum_m du
-// block = 384 threads = 96 column groups (8 columns) x 4 row phases; LDS reduction, 2x768 atomics per block
-template <typename T>
-__global__ void __launch_bounds__(384) scale_bwd_kernel(const float* __restrict__ dx, const T* __restrict__ u, const float* __restrict__ lam,
+// block = 4 * D/8 threads = D/8 column groups (8 columns) x 4 row phases; LDS reduction, 2 x D atomics per block
+template <typename T, int D>
+__global__ void __launch_bounds__(D / 2) scale_bwd_kernel(const float* __restrict__ dx, const T* __restrict__ u, const float* __restrict__ lam,
                                  T* __restrict__ du, float* __restrict__ ws, int M, int rows_per_block) {
-  __shared__ float red[384 * 8];
-  const int t = threadIdx.x, g = t % 96, ph = t / 96;
+  constexpr int NG = D / 8, NT = 4 * NG;
+  __shared__ float red[NT * 8];
+  const int t = threadIdx.x, g = t % NG, ph = t / NG;
   const int n = g * 8;
   int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
   float l[8]; load8<float>(lam + n, l);
@@ -238,38 +250,39 @@ __global__ void __launch_bounds__(384) scale_bwd_kernel(const float* __restrict_
 #pragma unroll 4
   for (int r = r0 + ph; r < r1; r += 4) {
     float d[8], uu[8], o[8];
-    load8<float>(dx + (long)r * 768 + n, d);
-    load8<T>(u + (long)r * 768 + n, uu);
+    load8<float>(dx + (long)r * D + n, d);
+    load8<T>(u + (long)r * D + n, uu);
 #pragma unroll
     for (int e = 0; e < 8; e++) { o[e] = d[e] * l[e]; sl[e] += d[e] * uu[e]; sb[e] += o[e]; }
-    store8<T>(du + (long)r * 768 + n, o);
+    store8<T>(du + (long)r * D + n, o);
   }
   for (int pass = 0; pass < 2; pass++) {
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < 8; e++) red[t * 8 + e] = pass ? sb[e] : sl[e];
     __syncthreads();
-    for (int c = t; c < 768; c += 384) {
+    for (int c = t; c < D; c += NT) {
       const int gg = c >> 3, e = c & 7;
       float s = 0.f;
 #pragma unroll
-      for (int q = 0; q < 4; q++) s += red[(q * 96 + gg) * 8 + e];
-      atomicAdd(ws + (long)(blockIdx.x % S3OD_NREP) * 1536 + (pass ? 768 : 0) + c, s);
+      for (int q = 0; q < 4; q++) s += red[(q * NG + gg) * 8 + e];
+      atomicAdd(ws + (long)(blockIdx.x % S3OD_NREP) * 2 * D + (pass ? D : 0) + c, s);
     }
   }
 }
 
-// dq,dk,dv [B,H,N,64] (dq w.r.t. the 1/8-scaled, rotated q) -> dqkv [B*N, 2304] T w.r.t. the
+// dq,dk,dv [B,H,N,64] (dq w.r.t. the 1/8-scaled, rotated q) -> dqkv [B*N, 3D] T w.r.t. the
 // pre-RoPE projections: d(pre) = cos*dy - R(sin*dy), R = rotate_half; dq additionally * 1/8.
 // Also accumulates the q / v bias gradients (column sums of dqkv; k_proj has no bias).
-// block = 288 threads = (which, head, 8-wide d chunk) x rows_per_block rows
-template <typename T>
-__global__ void __launch_bounds__(288) qkv_unrope_kernel(const T* __restrict__ dq, const T* __restrict__ dk, const T* __restrict__ dv,
+// block = 3 * H * 8 threads = (which, head, 8-wide d chunk) x rows_per_block rows
+template <typename T, int H>
+__global__ void __launch_bounds__(24 * H) qkv_unrope_kernel(const T* __restrict__ dq, const T* __restrict__ dk, const T* __restrict__ dv,
                                   const float* __restrict__ cs, const float* __restrict__ sn,
                                   T* __restrict__ dqkv, float* __restrict__ ws,
                                   int B, int Ntok, int P, int rows_per_block) {
+  constexpr int D = 64 * H;
   const int t = threadIdx.x;
-  const int d8 = t & 7, h = (t >> 3) % 12, which = t / 96;
+  const int d8 = t & 7, h = (t >> 3) % H, which = t / (8 * H);
   const int d0 = d8 * 8;
   const int pd = d0 < 32 ? d0 + 32 : d0 - 32;
   const T* src = which == 0 ? dq : (which == 1 ? dk : dv);
@@ -284,7 +297,7 @@ __global__ void __launch_bounds__(288) qkv_unrope_kernel(const T* __restrict__ d
     for (int j = 0; j < RB; j++) {
       const long m = min(m0 + j, r1 - 1);
       const int b = m / Ntok, tk = m - (long)b * Ntok;
-      const T* row = src + (((long)b * 12 + h) * Ntok + tk) * 64;
+      const T* row = src + (((long)b * H + h) * Ntok + tk) * 64;
       const int tp = max(tk - (Ntok - P), 0);
       rot[j] = which < 2 && tk >= Ntok - P;
       load8<T>(row + d0, v[j]);
@@ -305,41 +318,31 @@ __global__ void __launch_bounds__(288) qkv_unrope_kernel(const T* __restrict__ d
         if (which == 0) o[e] *= 0.125f;
         acc[e] += o[e];
       }
-      store8<T>(dqkv + m * 2304 + which * 768 + h * 64 + d0, o);
+      store8<T>(dqkv + m * 3 * D + which * D + h * 64 + d0, o);
     }
   }
-  if (which != 1 && ws) {   // replicated partials: ws[blk % NREP][q 768 | v 768]
-    float* dst = ws + (long)(blockIdx.x % S3OD_NREP) * 1536 + (which == 0 ? 0 : 768) + h * 64 + d0;
+  if (which != 1 && ws) {   // replicated partials: ws[blk % NREP][q D | v D]
+    float* dst = ws + (long)(blockIdx.x % S3OD_NREP) * 2 * D + (which == 0 ? 0 : D) + h * 64 + d0;
 #pragma unroll
     for (int e = 0; e < 8; e++) atomicAdd(dst + e, acc[e]);
   }
 }
 
-// out_q[i] += sum_r ws[r][i], out_v[i] += sum_r ws[r][768 + i]
-__global__ void qv_bias_fold_kernel(const float* __restrict__ ws, float* __restrict__ dbq, float* __restrict__ dbv) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 1536) return;
-  float s = 0.f;
-  for (int r = 0; r < S3OD_NREP; r++) s += ws[r * 1536 + i];
-  if (i < 768) { if (dbq) dbq[i] += s; }
-  else if (dbv) dbv[i - 768] += s;
-}
-
 // d(cls) = sum_b dx[b,0], d(reg[t]) = sum_b dx[b,1+t]  (accumulate)
-__global__ void token_prefix_bwd_kernel(const float* dx, float* dcls, float* dreg, int B, int Ntok) {
+__global__ void token_prefix_bwd_kernel(const float* dx, float* dcls, float* dreg, int B, int Ntok, int D) {
   int t = blockIdx.x;  // 0..4
-  float* dst = t == 0 ? dcls : dreg + (t - 1) * 768;
-  for (int c = threadIdx.x; c < 768; c += blockDim.x) {
+  float* dst = t == 0 ? dcls : dreg + (t - 1) * D;
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
     float s = 0.f;
-    for (int b = 0; b < B; b++) s += dx[((long)b * Ntok + t) * 768 + c];
+    for (int b = 0; b < B; b++) s += dx[((long)b * Ntok + t) * D + c];
     dst[c] += s;
   }
 }
 
 extern "C" {
 
-int s3od_token_prefix_bwd(const float* dx, float* dcls, float* dreg, int B, int Ntok, void* stream) {
-  hipLaunchKernelGGL(token_prefix_bwd_kernel, dim3(5), dim3(256), 0, (hipStream_t)stream, dx, dcls, dreg, B, Ntok);
+int s3od_token_prefix_bwd(const float* dx, float* dcls, float* dreg, int B, int Ntok, int D, void* stream) {
+  hipLaunchKernelGGL(token_prefix_bwd_kernel, dim3(5), dim3(256), 0, (hipStream_t)stream, dx, dcls, dreg, B, Ntok, D);
   return s3od_check_launch("token_prefix_bwd");
 }
 
@@ -352,8 +355,8 @@ int s3od_patch_im2col(int dtype, const float* x, void* cols, int B, int H, int W
   return s3od_check_launch("patch_im2col");
 }
 
-int s3od_token_prefix(float* x, const float* cls, const float* reg, int B, int Ntok, void* stream) {
-  hipLaunchKernelGGL(token_prefix_kernel, dim3(B, 5), dim3(256), 0, (hipStream_t)stream, x, cls, reg, Ntok);
+int s3od_token_prefix(float* x, const float* cls, const float* reg, int B, int Ntok, int D, void* stream) {
+  hipLaunchKernelGGL(token_prefix_kernel, dim3(B, 5), dim3(256), 0, (hipStream_t)stream, x, cls, reg, Ntok, D);
   return s3od_check_launch("token_prefix");
 }
 
@@ -363,30 +366,35 @@ int s3od_rope_table(float* cs, float* sn, int ph, int pw, float rescale, void* s
 }
 
 int s3od_layernorm_fwd(int dtype, const float* x, const float* w, const float* b, void* y, float* mean, float* rstd,
-                       int M, float eps, void* stream) {
-  DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(ln_fwd_kernel<T>, dim3(cdiv(M, 4)), dim3(256), 0, (hipStream_t)stream, x, w, b, (T*)y, mean, rstd, M, eps);
+                       int M, int D_, float eps, void* stream) {
+  DISPATCH_D(D_, {
+    DISPATCH_T(dtype, {
+      hipLaunchKernelGGL((ln_fwd_kernel<T, D>), dim3(cdiv(M, 4)), dim3(256), 0, (hipStream_t)stream, x, w, b, (T*)y, mean, rstd, M, eps);
+    });
   });
   return s3od_check_launch("layernorm_fwd");
 }
 
-// ws: workspace of S3OD_NREP * 1536 floats (replicated dw / db partials)
+// ws: workspace of S3OD_NREP * 2 * D floats (replicated dw / db partials)
 int s3od_layernorm_bwd(int dtype, const void* dy, const float* x, const float* mean, const float* rstd, const float* w,
-                       const float* dres, float* dx, float* dw, float* db, float* ws, int M, void* stream) {
+                       const float* dres, float* dx, float* dw, float* db, float* ws, int M, int D_, void* stream) {
   const int rpb = 64;
   hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(ws, 0, sizeof(float) * S3OD_NREP * 1536, st);
-  DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3(cdiv(M, rpb)), dim3(256), 0, st, (const T*)dy, x, mean, rstd, w, dres, dx, ws, M, rpb);
+  (void)hipMemsetAsync(ws, 0, sizeof(float) * S3OD_NREP * 2 * D_, st);
+  DISPATCH_D(D_, {
+    DISPATCH_T(dtype, {
+      hipLaunchKernelGGL((ln_bwd_kernel<T, D>), dim3(cdiv(M, rpb)), dim3(256), 0, st, (const T*)dy, x, mean, rstd, w, dres, dx, ws, M, rpb);
+    });
   });
-  hipLaunchKernelGGL(fold768x2_kernel, dim3(6), dim3(256), 0, st, ws, dw, db);
+  hipLaunchKernelGGL(fold2_kernel, dim3(cdiv(2 * D_, 256)), dim3(256), 0, st, ws, dw, db, D_);
   return s3od_check_launch("layernorm_bwd");
 }
 
-int s3od_cast_tap(int dtype, const float* x, void* y, int B, int Ntok, int P, void* stream) {
-  long total = (long)B * P * 768 / 8;
+int s3od_cast_tap(int dtype, const float* x, void* y, int B, int Ntok, int P, int D, void* stream) {
+  S3OD_REQUIRE(D % 8 == 0, "cast_tap: D %% 8");
+  long total = (long)B * P * D / 8;
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(cast_tap_kernel<T>, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream, x, (T*)y, B, Ntok, P);
+    hipLaunchKernelGGL(cast_tap_kernel<T>, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream, x, (T*)y, B, Ntok, P, D);
   });
   return s3od_check_launch("cast_tap");
 }
@@ -402,31 +410,40 @@ int s3od_colsum(int dtype, const void* a, long lda, int M, int N, float* out, vo
   return s3od_check_launch("colsum");
 }
 
-// ws: workspace of S3OD_NREP * 1536 floats (replicated dlam / dbias partials)
+// ws: workspace of S3OD_NREP * 2 * D floats (replicated dlam / dbias partials)
 int s3od_layerscale_bwd(int dtype, const float* dx, const void* u, const float* lam, void* du, float* dlam, float* dbias,
-                        float* ws, int M, void* stream) {
+                        float* ws, int M, int D_, void* stream) {
   const int rpb = 64;
   hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(ws, 0, sizeof(float) * S3OD_NREP * 1536, st);
-  DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(scale_bwd_kernel<T>, dim3(cdiv(M, rpb)), dim3(384), 0, st, dx, (const T*)u, lam, (T*)du, ws, M, rpb);
+  (void)hipMemsetAsync(ws, 0, sizeof(float) * S3OD_NREP * 2 * D_, st);
+  DISPATCH_D(D_, {
+    DISPATCH_T(dtype, {
+      hipLaunchKernelGGL((scale_bwd_kernel<T, D>), dim3(cdiv(M, rpb)), dim3(D / 2), 0, st, dx, (const T*)u, lam, (T*)du, ws, M, rpb);
+    });
   });
-  hipLaunchKernelGGL(fold768x2_kernel, dim3(6), dim3(256), 0, st, ws, dlam, dbias);
+  hipLaunchKernelGGL(fold2_kernel, dim3(cdiv(2 * D_, 256)), dim3(256), 0, st, ws, dlam, dbias, D_);
   return s3od_check_launch("layerscale_bwd");
 }
 
+// H heads of 64 (D = 64 H); ws: S3OD_NREP * 2 * D floats
 int s3od_qkv_unrope(int dtype, const void* dq, const void* dk, const void* dv, const float* cs, const float* sn,
-                    void* dqkv, float* dbq, float* dbv, float* ws, int B, int Ntok, int P, void* stream) {
+                    void* dqkv, float* dbq, float* dbv, float* ws, int B, int Ntok, int P, int H, void* stream) {
   S3OD_REQUIRE(ws || (!dbq && !dbv), "qkv_unrope: bias gradients need the workspace");
+  S3OD_REQUIRE(H == 12 || H == 16, "qkv_unrope: %d heads not built (12 or 16)", H);
   const long M = (long)B * Ntok;
+  const int D_ = 64 * H;
   const int rpb = dev_knob("S3OD_UNROPE_RPB", 64);
   hipStream_t st = (hipStream_t)stream;
-  if (ws) (void)hipMemsetAsync(ws, 0, sizeof(float) * S3OD_NREP * 1536, st);
+  if (ws) (void)hipMemsetAsync(ws, 0, sizeof(float) * S3OD_NREP * 2 * D_, st);
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(qkv_unrope_kernel<T>, dim3(cdiv(M, rpb)), dim3(288), 0, st, (const T*)dq, (const T*)dk,
-                       (const T*)dv, cs, sn, (T*)dqkv, ws, B, Ntok, P, rpb);
+    if (H == 12)
+      hipLaunchKernelGGL((qkv_unrope_kernel<T, 12>), dim3(cdiv(M, rpb)), dim3(24 * 12), 0, st, (const T*)dq, (const T*)dk,
+                         (const T*)dv, cs, sn, (T*)dqkv, ws, B, Ntok, P, rpb);
+    else
+      hipLaunchKernelGGL((qkv_unrope_kernel<T, 16>), dim3(cdiv(M, rpb)), dim3(24 * 16), 0, st, (const T*)dq, (const T*)dk,
+                         (const T*)dv, cs, sn, (T*)dqkv, ws, B, Ntok, P, rpb);
   });
-  if (ws) hipLaunchKernelGGL(qv_bias_fold_kernel, dim3(6), dim3(256), 0, st, ws, dbq, dbv);
+  if (ws) hipLaunchKernelGGL(fold2_kernel, dim3(cdiv(2 * D_, 256)), dim3(256), 0, st, ws, dbq, dbv, D_);
   return s3od_check_launch("qkv_unrope");
 }
 

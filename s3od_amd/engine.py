@@ -18,11 +18,10 @@ from dataclasses import dataclass, field
 import torch
 
 from ._lib import lib, stream, F32, BF16
-from .weights import N_LAYERS, TAPS, OUT_CH
+from .weights import OUT_CH, VARIANTS
 
-H_, D_, NREG = 12, 768, 4
+NREG = 4
 ACT_NONE, ACT_RELU, ACT_GELU, ACT_GELU_BWD, ACT_RELU_BWD = 0, 1, 2, 3, 4
-LAST_LAYER = max(TAPS)          # layers >= 11 (and the final norm) never reach the outputs
 
 
 def _E(ref, n, dt, dev):
@@ -41,10 +40,15 @@ class Ctx:
 
 
 class DPTEngine:
-    def __init__(self, params: dict, buffers: dict, compute_dtype: str = "bf16"):
-        """params / buffers: name -> fp32 CUDA tensor in the reference layout (canonical keys)."""
+    def __init__(self, params: dict, buffers: dict, compute_dtype: str = "bf16", variant: str = "dinob", n_masks: int = 3):
+        """params / buffers: name -> fp32 CUDA tensor in the reference layout (canonical keys).
+        variant: encoder geometry (weights.VARIANTS: dinob = ViT-B/16, dinol = ViT-L/16); n_masks: mask heads."""
         self.p = params
         self.buf = buffers
+        c = VARIANTS[variant]
+        self.D, self.H, self.MLP, self.taps = c.hidden, c.heads, c.mlp, c.taps
+        self.last = max(c.taps)      # layers >= last (and the final norm) never reach the outputs
+        self.nm = int(n_masks)
         self.set_dtype(compute_dtype)
         self.w = {}
         self._wkey = None
@@ -77,24 +81,25 @@ class DPTEngine:
             return out
 
         e = "encoder.embeddings."
-        w["pe"] = pack(e + "patch_embeddings.weight", D_, 3 * 16 * 16)
-        for i in range(LAST_LAYER):
+        D, MLP, nm = self.D, self.MLP, self.nm
+        w["pe"] = pack(e + "patch_embeddings.weight", D, 3 * 16 * 16)
+        for i in range(self.last):
             p = f"encoder.model.layer.{i}."
-            qkv = torch.empty((3 * D_, D_), dtype=T, device=dev)
-            pack(p + "attention.q_proj.weight", D_, D_, out=qkv[0:D_])
-            pack(p + "attention.k_proj.weight", D_, D_, out=qkv[D_:2 * D_])
-            pack(p + "attention.v_proj.weight", D_, D_, out=qkv[2 * D_:])
+            qkv = torch.empty((3 * D, D), dtype=T, device=dev)
+            pack(p + "attention.q_proj.weight", D, D, out=qkv[0:D])
+            pack(p + "attention.k_proj.weight", D, D, out=qkv[D:2 * D])
+            pack(p + "attention.v_proj.weight", D, D, out=qkv[2 * D:])
             w[f"qkv{i}"] = qkv
-            bq = torch.zeros(3 * D_, dtype=torch.float32, device=dev)
-            bq[:D_].copy_(P[p + "attention.q_proj.bias"])
-            bq[2 * D_:].copy_(P[p + "attention.v_proj.bias"])
+            bq = torch.zeros(3 * D, dtype=torch.float32, device=dev)
+            bq[:D].copy_(P[p + "attention.q_proj.bias"])
+            bq[2 * D:].copy_(P[p + "attention.v_proj.bias"])
             w[f"bqkv{i}"] = bq
-            w[f"o{i}"] = pack(p + "attention.o_proj.weight", D_, D_)
-            w[f"up{i}"] = pack(p + "mlp.up_proj.weight", 3072, D_)
-            w[f"down{i}"] = pack(p + "mlp.down_proj.weight", D_, 3072)
+            w[f"o{i}"] = pack(p + "attention.o_proj.weight", D, D)
+            w[f"up{i}"] = pack(p + "mlp.up_proj.weight", MLP, D)
+            w[f"down{i}"] = pack(p + "mlp.down_proj.weight", D, MLP)
         h = "seg_head."
         for i, c in enumerate(OUT_CH):
-            w[f"proj{i}"] = pack(h + f"projects.{i}.weight", c, D_)
+            w[f"proj{i}"] = pack(h + f"projects.{i}.weight", c, D)
         w["rs0"] = pack(h + "resize_layers.0.weight", 256, 256, 4, 4)   # ConvT: [Cin_T][Cout_T] = conv view
         w["rs1"] = pack(h + "resize_layers.1.weight", 512, 512, 2, 2)
         w["rs3"] = pack(h + "resize_layers.3.weight", 1024, 1024, 3, 3)
@@ -110,13 +115,13 @@ class DPTEngine:
         w["oc1"] = pack(m + "output_conv1.weight", 128, 256, 3, 3)
         w["up2x"] = pack(m + "upsample_2x.0.weight", 128, 64, 4, 4)     # ConvT [128][64][4][4]
         w["c64"] = pack(m + "upsample_2x.2.weight", 64, 64, 3, 3)
-        heads = torch.empty((96, 3, 3, 64), dtype=T, device=dev)
-        for k in range(3):
+        heads = torch.empty((32 * nm, 3, 3, 64), dtype=T, device=dev)
+        for k in range(nm):
             pack(m + f"mask_heads.{k}.0.weight", 32, 64, 3, 3, out=heads[32 * k:32 * (k + 1)])
         w["heads1"] = heads
-        w["heads1_b"] = torch.cat([P[m + f"mask_heads.{k}.0.bias"] for k in range(3)])
-        w["heads2"] = torch.cat([P[m + f"mask_heads.{k}.2.weight"].reshape(32) for k in range(3)])
-        w["heads2_b"] = torch.cat([P[m + f"mask_heads.{k}.2.bias"] for k in range(3)])
+        w["heads1_b"] = torch.cat([P[m + f"mask_heads.{k}.0.bias"] for k in range(nm)])
+        w["heads2"] = torch.cat([P[m + f"mask_heads.{k}.2.weight"].reshape(32) for k in range(nm)])
+        w["heads2_b"] = torch.cat([P[m + f"mask_heads.{k}.2.bias"] for k in range(nm)])
         self.w = w
         self._wkey = key
         L.phase = None
@@ -155,6 +160,7 @@ class DPTEngine:
     def encoder_forward(self, x, train=False, rope_rescale=None, ctx=None):
         lib().phase = "encoder"
         L, P, W8, dt, T = lib(), self.p, self.w, self.dt, self.tdt
+        D, H, MLP = self.D, self.H, self.MLP
         st = stream()
         B, _, Hh, Ww = x.shape
         ph, pw = Hh // 16, Ww // 16
@@ -165,55 +171,55 @@ class DPTEngine:
         cs = _E(None, (NP, 64), torch.float32, dev)
         sn = _E(None, (NP, 64), torch.float32, dev)
         L("s3od_rope_table", cs, sn, ph, pw, float(rope_rescale) if (train and rope_rescale) else -1.0, st)
-        cols = _E(None, (B * NP, D_), T, dev)
+        cols = _E(None, (B * NP, 768), T, dev)          # 3 x 16 x 16 patch pixels
         L("s3od_patch_im2col", dt, x, cols, B, Hh, Ww, st)
-        xs = _E(None, (B, Nt, D_), torch.float32, dev)
+        xs = _E(None, (B, Nt, D), torch.float32, dev)
         e = "encoder.embeddings."
-        self._lin(cols, W8["pe"], B * NP, D_, D_, xs, bias=P[e + "patch_embeddings.bias"], out_f32=True,
+        self._lin(cols, W8["pe"], B * NP, D, 768, xs, bias=P[e + "patch_embeddings.bias"], out_f32=True,
                   row_mode=1, P=NP, prefix=1 + NREG)
-        L("s3od_token_prefix", xs, P[e + "cls_token"], P[e + "register_tokens"], B, Nt, st)
+        L("s3od_token_prefix", xs, P[e + "cls_token"], P[e + "register_tokens"], B, Nt, D, st)
         if ctx is not None:
             ctx.t.update(cols=cols, cos=cs, sin=sn)
         taps = []
-        h1 = _E(None, (M, D_), T, dev)
-        q = _E(None, (B * H_, Nt, 64), T, dev)
+        h1 = _E(None, (M, D), T, dev)
+        q = _E(None, (B * H, Nt, 64), T, dev)
         k = torch.empty_like(q)
         v = torch.empty_like(q)
-        o = _E(None, (M, D_), T, dev)
-        a = _E(None, (M, 3072), T, dev)
-        for i in range(LAST_LAYER):
+        o = _E(None, (M, D), T, dev)
+        a = _E(None, (M, MLP), T, dev)
+        for i in range(self.last):
             p = f"encoder.model.layer.{i}."
             if ctx is not None:   # fresh buffers per layer for the backward
-                h1 = _E(None, (M, D_), T, dev); q = _E(None, (B * H_, Nt, 64), T, dev)
-                k = torch.empty_like(q); v = torch.empty_like(q); o = _E(None, (M, D_), T, dev)
-                a = _E(None, (M, 3072), T, dev)
+                h1 = _E(None, (M, D), T, dev); q = _E(None, (B * H, Nt, 64), T, dev)
+                k = torch.empty_like(q); v = torch.empty_like(q); o = _E(None, (M, D), T, dev)
+                a = _E(None, (M, MLP), T, dev)
                 mean1 = _E(None, (M,), torch.float32, dev); rstd1 = torch.empty_like(mean1)
                 mean2 = torch.empty_like(mean1); rstd2 = torch.empty_like(mean1)
-                lse = _E(None, (B * H_, Nt), torch.float32, dev)
-                u1 = _E(None, (M, D_), T, dev); u2 = _E(None, (M, D_), T, dev)
-                hpre = _E(None, (M, 3072), T, dev); h2 = _E(None, (M, D_), T, dev)
+                lse = _E(None, (B * H, Nt), torch.float32, dev)
+                u1 = _E(None, (M, D), T, dev); u2 = _E(None, (M, D), T, dev)
+                hpre = _E(None, (M, MLP), T, dev); h2 = _E(None, (M, D), T, dev)
             else:
                 mean1 = rstd1 = mean2 = rstd2 = _E(None, (M,), torch.float32, dev)
                 lse = None; u1 = u2 = hpre = None
                 h2 = h1
-            L("s3od_layernorm_fwd", dt, xs, P[p + "norm1.weight"], P[p + "norm1.bias"], h1, mean1, rstd1, M, 1e-5, st)
-            L("s3od_qkv_rope_fwd", dt, B, Nt, NP, h1, W8[f"qkv{i}"], W8[f"bqkv{i}"], cs, sn, q, k, v, st)
-            L("s3od_attn_fwd", dt, q, k, v, o, lse, B, H_, Nt, st)
-            xm = _E(None, (B, Nt, D_), torch.float32, dev)
-            self._lin(o, W8[f"o{i}"], M, D_, D_, xm, bias=P[p + "attention.o_proj.bias"],
+            L("s3od_layernorm_fwd", dt, xs, P[p + "norm1.weight"], P[p + "norm1.bias"], h1, mean1, rstd1, M, D, 1e-5, st)
+            L("s3od_qkv_rope_fwd", dt, B, Nt, NP, H, h1, W8[f"qkv{i}"], W8[f"bqkv{i}"], cs, sn, q, k, v, st)
+            L("s3od_attn_fwd", dt, q, k, v, o, lse, B, H, Nt, st)
+            xm = _E(None, (B, Nt, D), torch.float32, dev)
+            self._lin(o, W8[f"o{i}"], M, D, D, xm, bias=P[p + "attention.o_proj.bias"],
                       scale=P[p + "layer_scale1.lambda1"], res1=xs, res_f32=True, out_f32=True, pre=u1)
-            L("s3od_layernorm_fwd", dt, xm, P[p + "norm2.weight"], P[p + "norm2.bias"], h2, mean2, rstd2, M, 1e-5, st)
-            self._lin(h2, W8[f"up{i}"], M, 3072, D_, a, bias=P[p + "mlp.up_proj.bias"], act=ACT_GELU, pre=hpre)
-            xn = _E(None, (B, Nt, D_), torch.float32, dev)
-            self._lin(a, W8[f"down{i}"], M, D_, 3072, xn, bias=P[p + "mlp.down_proj.bias"],
+            L("s3od_layernorm_fwd", dt, xm, P[p + "norm2.weight"], P[p + "norm2.bias"], h2, mean2, rstd2, M, D, 1e-5, st)
+            self._lin(h2, W8[f"up{i}"], M, MLP, D, a, bias=P[p + "mlp.up_proj.bias"], act=ACT_GELU, pre=hpre)
+            xn = _E(None, (B, Nt, D), torch.float32, dev)
+            self._lin(a, W8[f"down{i}"], M, D, MLP, xn, bias=P[p + "mlp.down_proj.bias"],
                       scale=P[p + "layer_scale2.lambda1"], res1=xm, res_f32=True, out_f32=True, pre=u2)
             if ctx is not None:
                 ctx.t[f"L{i}"] = dict(x=xs, h1=h1, mean1=mean1, rstd1=rstd1, q=q, k=k, v=v, o=o, lse=lse, u1=u1,
                                       xm=xm, h2=h2, mean2=mean2, rstd2=rstd2, hpre=hpre, a=a, u2=u2)
             xs = xn
-            if i + 1 in TAPS:
-                tp = _E(None, (B, NP, D_), T, dev)
-                L("s3od_cast_tap", dt, xs, tp, B, Nt, NP, st)
+            if i + 1 in self.taps:
+                tp = _E(None, (B, NP, D), T, dev)
+                L("s3od_cast_tap", dt, xs, tp, B, Nt, NP, D, st)
                 taps.append(tp)
         return taps, (B, ph, pw, Nt)
 
@@ -291,7 +297,7 @@ class DPTEngine:
         proj = []
         for i, c in enumerate(OUT_CH):
             y = torch.empty((B, ph, pw, c), dtype=self.tdt, device=dev)
-            self._lin(taps[i], W8[f"proj{i}"], B * NP, c, D_, y, bias=P[h + f"projects.{i}.bias"])
+            self._lin(taps[i], W8[f"proj{i}"], B * NP, c, self.D, y, bias=P[h + f"projects.{i}.bias"])
             proj.append(y)
         f0 = self._convT(proj[0], W8["rs0"], B, ph, pw, 256, 256, 4, 4, 0, bias=P[h + "resize_layers.0.bias"])
         f1 = self._convT(proj[1], W8["rs1"], B, ph, pw, 512, 512, 2, 2, 0, bias=P[h + "resize_layers.1.bias"])
@@ -311,9 +317,10 @@ class DPTEngine:
         pooled = torch.empty((B, 256), dtype=torch.float32, device=dev)
         L("s3od_avgpool", dt, p1, pooled, B, H1 * W1, 256, st)
         hid = torch.empty((B, 64), dtype=torch.float32, device=dev)
-        iou = torch.empty((B, 3), dtype=torch.float32, device=dev)
+        nm = self.nm
+        iou = torch.empty((B, nm), dtype=torch.float32, device=dev)
         L("s3od_iou_head_fwd", pooled, P[h + "classifier_head.2.weight"], P[h + "classifier_head.2.bias"],
-          P[h + "classifier_head.4.weight"], P[h + "classifier_head.4.bias"], hid, iou, B, st)
+          P[h + "classifier_head.4.weight"], P[h + "classifier_head.4.bias"], hid, iou, B, nm, st)
         # mask head (src/s3od/model.py:455-467)
         m = h + "mask_head."
         oc1 = self._conv(p1, W8["oc1"], B, H1, W1, 256, 128, 3, 1, 1, bias=P[m + "output_conv1.bias"])
@@ -322,9 +329,9 @@ class DPTEngine:
         c64 = self._conv(up, W8["c64"], B, HH, WW, 64, 64, 3, 1, 1, bias=P[m + "upsample_2x.2.bias"], act=ACT_RELU)
         # F.interpolate(size=(16ph,16pw), antialias=True) is an exact identity here (HH == 16*ph)
         assert HH == 16 * ph and WW == 16 * pw
-        logits = torch.empty((B, 3, HH, WW), dtype=torch.float32, device=dev)
-        hsave = torch.empty((B * HH * WW, 96), dtype=self.tdt, device=dev) if ctx is not None else None
-        L("s3od_mask_heads_fwd", dt, B, HH, WW, c64, W8["heads1"], W8["heads1_b"], W8["heads2"], W8["heads2_b"],
+        logits = torch.empty((B, nm, HH, WW), dtype=torch.float32, device=dev)
+        hsave = torch.empty((B * HH * WW, 32 * nm), dtype=self.tdt, device=dev) if ctx is not None else None
+        L("s3od_mask_heads_fwd", dt, B, HH, WW, nm, c64, W8["heads1"], W8["heads1_b"], W8["heads2"], W8["heads2_b"],
           logits, hsave, st)
         if ctx is not None:
             ctx.t["head"] = dict(p1=p1, pooled=pooled, hid=hid, oc1=oc1, up=up, c64=c64, hsave=hsave)
@@ -433,13 +440,14 @@ class DPTEngine:
         H1, W1 = p1.shape[1], p1.shape[2]
         HH, WW = up.shape[1], up.shape[2]
         npx = B * HH * WW
-        # ---- three mask heads
-        dh = torch.empty((npx, 96), dtype=self.tdt, device=dev)
+        # ---- the mask heads (fused, N = 32 * n_masks)
+        nm = self.nm
+        dh = torch.empty((npx, 32 * nm), dtype=self.tdt, device=dev)
         L("s3od_mask_heads_bwd", dt, d_logits.contiguous(), hd["hsave"], W8["heads2"], dh, G["heads2_w"], G["heads2_b"],
-          G["heads1_b"], B, HH * WW, st)
-        self._wgrad_conv(dh, c64, B, HH, WW, 64, HH, WW, 96, 3, 1, 1, G["heads1_w"])
+          G["heads1_b"], B, HH * WW, nm, st)
+        self._wgrad_conv(dh, c64, B, HH, WW, 64, HH, WW, 32 * nm, 3, 1, 1, G["heads1_w"])
         # (bias gradients are column sums fused into the epilogue that produces each gradient)
-        d64 = self._dgrad_conv(dh, W8["heads1"], B, HH, WW, 64, HH, WW, 96, 3, 1, 1, act=ACT_RELU_BWD, res1=c64,
+        d64 = self._dgrad_conv(dh, W8["heads1"], B, HH, WW, 64, HH, WW, 32 * nm, 3, 1, 1, act=ACT_RELU_BWD, res1=c64,
                                colsum=G[m + "upsample_2x.2.bias"])
         # ---- upsample_2x.2 conv 64->64 + ReLU
         self._wgrad_conv(d64, up, B, HH, WW, 64, HH, WW, 64, 3, 1, 1, G[m + "upsample_2x.2.weight"])
@@ -455,7 +463,7 @@ class DPTEngine:
         dpix = torch.empty((B, 256), dtype=torch.float32, device=dev)
         L("s3od_iou_head_bwd", hd["pooled"], hd["hid"], P[h + "classifier_head.2.weight"], P[h + "classifier_head.4.weight"],
           d_iou.contiguous(), G[h + "classifier_head.2.weight"], G[h + "classifier_head.2.bias"],
-          G[h + "classifier_head.4.weight"], G[h + "classifier_head.4.bias"], dpix, B, H1 * W1, st)
+          G[h + "classifier_head.4.weight"], G[h + "classifier_head.4.bias"], dpix, B, H1 * W1, nm, st)
         # ---- refinenets
         dp2, drn1 = self._fusion_bwd(1, dp1, B, ctx, G, bcast=dpix)
         dp3, drn2 = self._fusion_bwd(2, dp2, B, ctx, G)
@@ -487,7 +495,7 @@ class DPTEngine:
         NP = ph * pw
         dtaps = []
         for i, c in enumerate(OUT_CH):
-            self._wgrad_lin(dproj[i], dec["taps"][i], c, D_, B * NP, G[h + f"projects.{i}.weight"])
+            self._wgrad_lin(dproj[i], dec["taps"][i], c, self.D, B * NP, G[h + f"projects.{i}.weight"])
             dtaps.append((dproj[i], c))
         lib().phase = None
         return dtaps
@@ -495,68 +503,69 @@ class DPTEngine:
     def encoder_backward(self, ctx, dtaps, G):
         lib().phase = "encoder"
         L, P, W8, dt, T = lib(), self.p, self.w, self.dt, self.tdt
+        D, H, MLP = self.D, self.H, self.MLP
         st = stream()
         B, ph, pw = ctx.B, ctx.ph, ctx.pw
         NP = ph * pw
         Nt = NP + 1 + NREG
         M = B * Nt
         dev = dtaps[0][0].device
-        dx = torch.zeros((B, Nt, D_), dtype=torch.float32, device=dev)
-        tap_of = {t: j for j, t in enumerate(TAPS)}
-        du = _E(None, (M, D_), T, dev)
-        dhp = _E(None, (M, 3072), T, dev)
-        dh = _E(None, (M, D_), T, dev)
-        dxm = _E(None, (B, Nt, D_), torch.float32, dev)
-        dxi = _E(None, (B, Nt, D_), torch.float32, dev)
-        dqkv = _E(None, (M, 3 * D_), T, dev)
-        dq = _E(None, (B * H_, Nt, 64), T, dev)
+        dx = torch.zeros((B, Nt, D), dtype=torch.float32, device=dev)
+        tap_of = {t: j for j, t in enumerate(self.taps)}
+        du = _E(None, (M, D), T, dev)
+        dhp = _E(None, (M, MLP), T, dev)
+        dh = _E(None, (M, D), T, dev)
+        dxm = _E(None, (B, Nt, D), torch.float32, dev)
+        dxi = _E(None, (B, Nt, D), torch.float32, dev)
+        dqkv = _E(None, (M, 3 * D), T, dev)
+        dq = _E(None, (B * H, Nt, 64), T, dev)
         dk = torch.empty_like(dq)
         dv = torch.empty_like(dq)
-        delta = _E(None, (B * H_, Nt), torch.float32, dev)
-        qv_ws = _E(None, (32 * 1536,), torch.float32, dev)      # S3OD_NREP replicas of the q/v bias partials
-        red_ws = _E(None, (32 * 1536,), torch.float32, dev)     # same, for LayerNorm / LayerScale parameter grads
-        for i in reversed(range(LAST_LAYER)):
+        delta = _E(None, (B * H, Nt), torch.float32, dev)
+        qv_ws = _E(None, (32 * 2 * D,), torch.float32, dev)     # S3OD_NREP replicas of the q/v bias partials
+        red_ws = _E(None, (32 * 2 * D,), torch.float32, dev)    # same, for LayerNorm / LayerScale parameter grads
+        for i in reversed(range(self.last)):
             if i + 1 in tap_of:
                 dp, c = dtaps[tap_of[i + 1]]
                 # dx[prefix-skipped rows] += dproj @ W_proj   (in-place accumulate, fp32)
-                self._dgrad_lin(dp, W8[f"proj{tap_of[i + 1]}"], B * NP, D_, c, dx, aux=dx, out_f32=True,
-                                row_mode=1, P=NP, prefix=1 + NREG, ldaux=D_)
+                self._dgrad_lin(dp, W8[f"proj{tap_of[i + 1]}"], B * NP, D, c, dx, aux=dx, out_f32=True,
+                                row_mode=1, P=NP, prefix=1 + NREG, ldaux=D)
             p = f"encoder.model.layer.{i}."
             s = ctx.t[f"L{i}"]
             # ---- MLP half
             L("s3od_layerscale_bwd", dt, dx, s["u2"], P[p + "layer_scale2.lambda1"], du, G[p + "layer_scale2.lambda1"],
-              G[p + "mlp.down_proj.bias"], red_ws, M, st)
-            self._wgrad_lin(du, s["a"], D_, 3072, M, G[p + "mlp.down_proj.weight"])
-            self._dgrad_lin(du, W8[f"down{i}"], M, 3072, D_, dhp, act=ACT_GELU_BWD, aux=s["hpre"],
+              G[p + "mlp.down_proj.bias"], red_ws, M, D, st)
+            self._wgrad_lin(du, s["a"], D, MLP, M, G[p + "mlp.down_proj.weight"])
+            self._dgrad_lin(du, W8[f"down{i}"], M, MLP, D, dhp, act=ACT_GELU_BWD, aux=s["hpre"],
                             colsum=G[p + "mlp.up_proj.bias"])
-            self._wgrad_lin(dhp, s["h2"], 3072, D_, M, G[p + "mlp.up_proj.weight"])
-            self._dgrad_lin(dhp, W8[f"up{i}"], M, D_, 3072, dh)
+            self._wgrad_lin(dhp, s["h2"], MLP, D, M, G[p + "mlp.up_proj.weight"])
+            self._dgrad_lin(dhp, W8[f"up{i}"], M, D, MLP, dh)
             L("s3od_layernorm_bwd", dt, dh, s["xm"], s["mean2"], s["rstd2"], P[p + "norm2.weight"], dx, dxm,
-              G[p + "norm2.weight"], G[p + "norm2.bias"], red_ws, M, st)
+              G[p + "norm2.weight"], G[p + "norm2.bias"], red_ws, M, D, st)
             # ---- attention half
             L("s3od_layerscale_bwd", dt, dxm, s["u1"], P[p + "layer_scale1.lambda1"], du, G[p + "layer_scale1.lambda1"],
-              G[p + "attention.o_proj.bias"], red_ws, M, st)
-            self._wgrad_lin(du, s["o"], D_, D_, M, G[p + "attention.o_proj.weight"])
+              G[p + "attention.o_proj.bias"], red_ws, M, D, st)
+            self._wgrad_lin(du, s["o"], D, D, M, G[p + "attention.o_proj.weight"])
             do = dh
-            self._dgrad_lin(du, W8[f"o{i}"], M, D_, D_, do)
-            L("s3od_attn_bwd", dt, s["q"], s["k"], s["v"], s["o"], do, s["lse"], delta, dq, dk, dv, B, H_, Nt, st)
+            self._dgrad_lin(du, W8[f"o{i}"], M, D, D, do)
+            L("s3od_attn_bwd", dt, s["q"], s["k"], s["v"], s["o"], do, s["lse"], delta, dq, dk, dv, B, H, Nt, st)
             L("s3od_qkv_unrope", dt, dq, dk, dv, ctx.t["cos"], ctx.t["sin"], dqkv, G[p + "attention.q_proj.bias"],
-              G[p + "attention.v_proj.bias"], qv_ws, B, Nt, NP, st)
-            self._wgrad_lin(dqkv, s["h1"], 3 * D_, D_, M, G[f"qkv_w{i}"])
+              G[p + "attention.v_proj.bias"], qv_ws, B, Nt, NP, H, st)
+            self._wgrad_lin(dqkv, s["h1"], 3 * D, D, M, G[f"qkv_w{i}"])
             dh1 = dh
-            self._dgrad_lin(dqkv, W8[f"qkv{i}"], M, D_, 3 * D_, dh1)
+            self._dgrad_lin(dqkv, W8[f"qkv{i}"], M, D, 3 * D, dh1)
             L("s3od_layernorm_bwd", dt, dh1, s["x"], s["mean1"], s["rstd1"], P[p + "norm1.weight"], dxm, dxi,
-              G[p + "norm1.weight"], G[p + "norm1.bias"], red_ws, M, st)
+              G[p + "norm1.weight"], G[p + "norm1.bias"], red_ws, M, D, st)
             dx, dxi = dxi, dx
             if self.grad_hook is not None:
                 self.grad_hook(f"layer{i}")
         # ---- embeddings
         e = "encoder.embeddings."
-        L("s3od_token_prefix_bwd", dx, G[e + "cls_token"], G[e + "register_tokens"], B, Nt, st)
-        dpatch = _E(None, (B, NP, D_), T, dev)
-        L("s3od_cast_tap", dt, dx, dpatch, B, Nt, NP, st)
-        self._colsum(dpatch, B * NP, D_, G[e + "patch_embeddings.bias"])
-        self._wgrad_lin(dpatch, ctx.t["cols"], D_, D_, B * NP, G[e + "patch_embeddings.weight"])
+        L("s3od_token_prefix_bwd", dx, G[e + "cls_token"], G[e + "register_tokens"], B, Nt, D, st)
+        dpatch = _E(None, (B, NP, D), T, dev)
+        L("s3od_cast_tap", dt, dx, dpatch, B, Nt, NP, D, st)
+        self._colsum(dpatch, B * NP, D, G[e + "patch_embeddings.bias"])
+        self._wgrad_lin(dpatch, ctx.t["cols"], D, 768, B * NP, G[e + "patch_embeddings.weight"])
         lib().phase = None
         if self.grad_hook is not None:
             self.grad_hook("embeddings")

@@ -61,7 +61,7 @@ class LossModule(nn.Module):
     def forward(self, outputs, targets, epoch: int):
         pm = outputs["pred_masks"]
         if pm.size(1) == 1:
-            raise NotImplementedError("single-mask branch (loss.py:166-188) is the dinol variant; not built")
+            return self._single_mask(pm, outputs["pred_iou"], targets)
         lam = self.full_mask_lambda * math.exp(-self.decay_rate * epoch)
         cfg = {"w_focal": self.w["focal"], "w_iou": self.w["iou"], "w_bce": self.w["bce"], "w_ssim": self.w["ssim"],
                "w_mse": self.w["mse"], "lam": lam}
@@ -77,6 +77,27 @@ class LossModule(nn.Module):
             parts[self._names["mse"]] = packed[3]
         self.last_gt_ious = packed[16:16 + B * M].view(B, M)
         self.last_best = packed[16 + B * M:16 + B * M + B]
+        return loss, parts
+
+
+    def _single_mask(self, pm, pred_iou, targets):
+        """MaskLossHandler.compute_single_mask_loss (loss.py:166-188; the dinol config, num_outputs=1):
+        loss = sum_c w_c * mean(criterion_c(sigmoid(logits), masks)) over the [B,H,W] maps; no best-mask
+        selection, no decayed all-mask term and no aux MSE (pred_iou gets no gradient).  This is the fused
+        multi-mask kernel at M=1 with lambda=0 and w_mse=0.  Returns parts {criterion name: value}."""
+        if self.w["ssim"]:
+            # SSIMLoss(reduction='none') on a [B,H,W] map: F.conv2d reads it as unbatched [C=B,H,W] and
+            # .mean((1,2,3)) has no dim 3 -- the reference raises here for every batch size
+            raise RuntimeError("SSIMLoss on the single-mask [B,H,W] maps fails in the reference (loss.py:176-179, :74-75)")
+        cfg = {"w_focal": self.w["focal"], "w_iou": self.w["iou"], "w_bce": self.w["bce"], "w_ssim": 0.0, "w_mse": 0.0,
+               "lam": 0.0}
+        loss, packed = mask_loss(pm, pred_iou.detach(), targets["masks"], cfg)
+        parts = {}
+        for ci, kind in enumerate(("focal", "iou", "bce")):
+            if kind in self._names:
+                parts[self._names[kind]] = packed[4 + 2 * ci]
+        self.last_gt_ious = packed[16:16 + pm.shape[0]].view(-1, 1)
+        self.last_best = None
         return loss, parts
 
 

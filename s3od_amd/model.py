@@ -18,9 +18,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from .weights import param_specs, synthetic_state_dict, canonicalize_state_dict
-
-_ENCODERS = {"dinov3_base", "facebook/dinov3-vitb16-pretrain-lvd1689m", "dinob"}
+from .weights import param_specs, synthetic_state_dict, canonicalize_state_dict, ENCODER_VARIANT, VARIANTS
 
 
 def _container():
@@ -51,24 +49,29 @@ def _build_tree(root: nn.Module, specs):
 
 
 class DPTSegmentation(nn.Module):
-    """DINOv3 ViT-B/16 + DPT head + 3-way MultiMaskHead on MI355X HIP kernels."""
+    """DINOv3 ViT-B/16 (dinob) or ViT-L/16 (dinol) + DPT head + MultiMaskHead on MI355X HIP kernels."""
 
     def __init__(self, num_classes=1, num_outputs=3, encoder_name="dinov3_base", features=256, out_channels=None,
                  use_bn=True, use_clstoken=False, compute_dtype="bf16", init_seed=0, **kwargs):
         super().__init__()
-        if num_classes != 1 or num_outputs != 3 or features != 256 or not use_bn or use_clstoken:
-            raise NotImplementedError("only the published S3OD configuration (dinob, 3 masks, 256 features, BN) is built")
+        if num_classes != 1 or features != 256 or not use_bn or use_clstoken:
+            raise NotImplementedError("only the published S3OD head configuration (1 class, 256 features, BN, "
+                                      "no cls-token readout) is built")
+        if num_outputs not in (1, 3):
+            raise NotImplementedError(f"num_outputs={num_outputs}: the fused mask-head kernels are built for 1 (dinol) or 3 (dinob)")
         if out_channels not in (None, [256, 512, 1024, 1024], (256, 512, 1024, 1024)):
             raise NotImplementedError("out_channels must be [256, 512, 1024, 1024]")
-        if encoder_name not in _ENCODERS:
-            raise NotImplementedError(f"encoder {encoder_name!r}: only ViT-B/16 (dinov3_base) is built")
+        if encoder_name not in ENCODER_VARIANT:
+            raise NotImplementedError(f"encoder {encoder_name!r}: ViT-B/16 (dinob) and ViT-L/16 (dinol) are built")
         self.patch_size = 16
         self.encoder_name = encoder_name
+        self.variant = ENCODER_VARIANT[encoder_name]
+        self.num_outputs = int(num_outputs)
         self.use_flux_features = False
         self.compute_dtype = compute_dtype
-        _build_tree(self, param_specs())
+        _build_tree(self, param_specs(self.variant, self.num_outputs))
         if init_seed is not None:
-            sd = synthetic_state_dict(init_seed)
+            sd = synthetic_state_dict(init_seed, self.variant, self.num_outputs)
             with torch.no_grad():
                 own = self.state_dict(keep_vars=True)
                 for k, v in sd.items():
@@ -94,7 +97,7 @@ class DPTSegmentation(nn.Module):
         e = self._engine
         if e is None or e.p.keys() != params.keys() or any(e.p[k] is not v for k, v in params.items()) or \
                 any(e.buf[k] is not v for k, v in bufs.items()):
-            e = DPTEngine(params, bufs, self.compute_dtype)
+            e = DPTEngine(params, bufs, self.compute_dtype, self.variant, self.num_outputs)
             self._engine = e
         if e.cdt != self.compute_dtype:
             e.set_dtype(self.compute_dtype)
@@ -105,8 +108,8 @@ class DPTSegmentation(nn.Module):
         """Flat gradient order: reference order with q/k/v weights and the three mask heads'
         weights/biases made adjacent (they are produced by single fused kernels), encoder first.
         Returns (list of (name, numel, shape), dict range_name -> (start, end))."""
-        from .weights import N_LAYERS
-        specs = [(n, sh) for n, sh, k in param_specs() if not (k.startswith("bn_") and k not in ("bn_w", "bn_b"))]
+        nm = self.num_outputs
+        specs = [(n, sh) for n, sh, k in param_specs(self.variant, nm) if not (k.startswith("bn_") and k not in ("bn_w", "bn_b"))]
         shapes = dict(specs)
         unused = set(self.unused_parameter_names())
         order = []
@@ -122,7 +125,7 @@ class DPTSegmentation(nn.Module):
             elif ".mask_heads." in n:
                 m = "seg_head.mask_head.mask_heads."
                 grp = [m + f"{k}.{a}.{b}" for a, b in (("0", "weight"), ("0", "bias"), ("2", "weight"), ("2", "bias"))
-                       for k in range(3)]
+                       for k in range(nm)]
                 grp = [g for g in grp if g not in done]
             else:
                 grp = [n]
@@ -139,13 +142,15 @@ class DPTSegmentation(nn.Module):
             off += numel
         return layout, ranges, off
 
-    @staticmethod
-    def unused_parameter_names():
-        from .weights import N_LAYERS
-        last = N_LAYERS - 1
-        names = [n for n, sh, k in param_specs() if n.startswith(f"encoder.model.layer.{last}.")]
+    def unused_parameter_names(self):
+        """Parameters the reference's forward never reaches (grad stays None): encoder layers at and
+        after the last tap (dinob: layer 11; dinol: layer 23), the final norm, mask_token and
+        refinenet4.resConfUnit1."""
+        last = max(VARIANTS[self.variant].taps)
+        specs = param_specs(self.variant, self.num_outputs)
+        names = [n for n, sh, k in specs if n.startswith("encoder.model.layer.") and int(n.split(".")[3]) >= last]
         names += ["encoder.norm.weight", "encoder.norm.bias", "encoder.embeddings.mask_token"]
-        names += [n for n, sh, k in param_specs() if n.startswith("seg_head.scratch.refinenet4.resConfUnit1.")
+        names += [n for n, sh, k in specs if n.startswith("seg_head.scratch.refinenet4.resConfUnit1.")
                   and not (k.startswith("bn_") and k not in ("bn_w", "bn_b"))]
         return names
 
@@ -189,13 +194,14 @@ class DPTSegmentation(nn.Module):
                 p.grad = v
             G[n] = v
         pos = {n: off for n, off, numel, shape in fl["layout"]}
-        for i in range(11):
+        V, nm = VARIANTS[self.variant], self.num_outputs
+        for i in range(max(V.taps)):
             q = f"encoder.model.layer.{i}.attention."
             o = pos[q + "q_proj.weight"]
-            G[f"qkv_w{i}"] = buf[o:o + 3 * 768 * 768]
+            G[f"qkv_w{i}"] = buf[o:o + 3 * V.hidden * V.hidden]
         m = "seg_head.mask_head.mask_heads."
-        for key, n, cnt in (("heads1_w", "0.0.weight", 96 * 64 * 9), ("heads1_b", "0.0.bias", 96),
-                            ("heads2_w", "0.2.weight", 96), ("heads2_b", "0.2.bias", 3)):
+        for key, n, cnt in (("heads1_w", "0.0.weight", 32 * nm * 64 * 9), ("heads1_b", "0.0.bias", 32 * nm),
+                            ("heads2_w", "0.2.weight", 32 * nm), ("heads2_b", "0.2.bias", nm)):
             o = pos[m + n]
             G[key] = buf[o:o + cnt]
         return G

@@ -16,7 +16,7 @@ layout: ``src/s3od/dinov3_config/config.json:29``) and Lightning ``model.``-pref
 from __future__ import annotations
 
 import zlib
-from collections import OrderedDict
+from collections import OrderedDict, namedtuple
 
 import numpy as np
 
@@ -32,13 +32,31 @@ OUT_CH = (256, 512, 1024, 1024)  # src/s3od/model.py:45
 FEAT = 256
 N_MASKS = 3
 
+# Encoder geometries of the two published model configs (synth_sod/.../config/model/{dinob,dinol}.yaml):
+#   dinob: facebook/dinov3-vitb16-pretrain-lvd1689m (src/s3od/dinov3_config/config.json: hidden 768,
+#          12 layers, 12 heads, intermediate 3072), taps [2,5,8,11] (MT/model.py:28-32);
+#   dinol: facebook/dinov3-vitl16-pretrain-lvd1689m (transformers' DINOv3ViT-L/16 geometry: hidden 1024,
+#          24 layers, 16 heads of 64, intermediate 4096, 4 registers, same RoPE / LayerScale / key_bias=False),
+#          taps [4,11,17,23] (MT/model.py:28-32).  Its config file is not in the reference tree.
+Variant = namedtuple("Variant", "hidden layers heads mlp taps")
+VARIANTS = {
+    "dinob": Variant(768, 12, 12, 3072, (2, 5, 8, 11)),
+    "dinol": Variant(1024, 24, 16, 4096, (4, 11, 17, 23)),
+}
+ENCODER_VARIANT = {
+    "dinov3_base": "dinob", "dinob": "dinob", "facebook/dinov3-vitb16-pretrain-lvd1689m": "dinob",
+    "dinov3_large": "dinol", "dinol": "dinol", "facebook/dinov3-vitl16-pretrain-lvd1689m": "dinol",
+}
 
-def param_specs():
+
+def param_specs(variant: str = "dinob", n_masks: int = N_MASKS):
     """Ordered (name, shape, kind) for every state-dict entry of DPTSegmentation.
 
     kind drives the synthetic init: 'lin' (fan-in scaled normal), 'bias', 'ln_w', 'ln_b',
     'ls' (LayerScale), 'tok', 'zero', 'bn_w', 'bn_b', 'bn_rm', 'bn_rv', 'bn_nbt', 'convT'.
     """
+    V = VARIANTS[variant]
+    HIDDEN, MLP, N_LAYERS, N_MASKS = V.hidden, V.mlp, V.layers, n_masks
     s = []
     e = "encoder.embeddings."
     s += [(e + "cls_token", (1, 1, HIDDEN), "tok"),
@@ -96,7 +114,7 @@ def param_specs():
         s += [(m + f"mask_heads.{k}.0.weight", (32, 64, 3, 3), "lin"), (m + f"mask_heads.{k}.0.bias", (32,), "bias"),
               (m + f"mask_heads.{k}.2.weight", (1, 32, 1, 1), "head"), (m + f"mask_heads.{k}.2.bias", (1,), "bias")]
     s += [(h + "classifier_head.2.weight", (64, 256), "lin"), (h + "classifier_head.2.bias", (64,), "bias"),
-          (h + "classifier_head.4.weight", (3, 64), "lin"), (h + "classifier_head.4.bias", (3,), "bias")]
+          (h + "classifier_head.4.weight", (N_MASKS, 64), "lin"), (h + "classifier_head.4.bias", (N_MASKS,), "bias")]
     return s
 
 
@@ -141,8 +159,8 @@ def synthetic_tensor(name: str, shape, kind: str, seed: int = 0) -> np.ndarray:
     raise ValueError(kind)
 
 
-def synthetic_state_dict(seed: int = 0) -> "OrderedDict[str, np.ndarray]":
-    return OrderedDict((n, synthetic_tensor(n, sh, k, seed)) for n, sh, k in param_specs())
+def synthetic_state_dict(seed: int = 0, variant: str = "dinob", n_masks: int = N_MASKS) -> "OrderedDict[str, np.ndarray]":
+    return OrderedDict((n, synthetic_tensor(n, sh, k, seed)) for n, sh, k in param_specs(variant, n_masks))
 
 
 def canonicalize_state_dict(sd):

@@ -215,8 +215,89 @@ def gen_losses(seed=5):
     print("losses done")
 
 
+def build_reference_dinol(seed=0):
+    """The reference's DPTSegmentation with encoder_name="dinov3_large" (taps [4,11,17,23]) and
+    num_outputs=1 (config/model/dinol.yaml).  The reference ships only the ViT-B config file
+    (src/s3od/dinov3_config/config.json), so AutoConfig is substituted by that same config with
+    transformers' DINOv3 ViT-L/16 geometry (hidden 1024, 24 layers, 16 heads, intermediate 4096);
+    everything else (RoPE, LayerScale, key_bias=False, registers, the DPT head) is the reference code."""
+    import json
+    import s3od.model as M
+    from transformers import DINOv3ViTConfig
+    base = json.load(open(REF / "src" / "s3od" / "dinov3_config" / "config.json"))
+    base = {k: v for k, v in base.items() if k not in ("architectures", "model_type", "transformers_version", "torch_dtype")}
+    base.update(hidden_size=1024, num_hidden_layers=24, num_attention_heads=16, intermediate_size=4096)
+    cfg = DINOv3ViTConfig(**base)
+    M.AutoImageProcessor = types.SimpleNamespace(from_pretrained=lambda *a, **k: None)
+    M.AutoConfig = types.SimpleNamespace(from_pretrained=lambda *a, **k: cfg)
+    m = M.DPTSegmentation(num_classes=1, num_outputs=1, encoder_name="dinov3_large")
+    sd = {k: torch.from_numpy(v) for k, v in synthetic_state_dict(seed, "dinol", 1).items()}
+    m.load_state_dict(sd, strict=True)
+    return m
+
+
+def gen_dinol(seed=7, rescale=0.83):
+    """dinol goldens: eval forward at 128x160 bs=1 and one train step at 128^2 bs=2 with the
+    single-mask loss (loss.py:166-188, focal_iou criterions) -> tests/golden/dinol.npz."""
+    import transformers.models.dinov3_vit.modeling_dinov3_vit as D
+    from synth_sod.model_training.loss import LossModule
+    m = build_reference_dinol(0).eval()
+    out = {}
+    x = seeded_images(1, 128, 160, seed)
+    with torch.no_grad():
+        o = m(x)
+    out.update(fwd_x=x.numpy(), fwd_pred_masks=o["pred_masks"].numpy(), fwd_pred_iou=o["pred_iou"].numpy(),
+               fwd_features_sub=o["features"][:, :, ::4, ::4].numpy())
+    orig = D.augment_patches_center_coordinates
+    D.augment_patches_center_coordinates = lambda coords, shift=None, jitter=None, rescale_=None, **k: coords * rescale
+    try:
+        crit = [
+            {"name": "focal_loss", "target_key": "masks", "output_key": "pred_masks", "weight": 20,
+             "loss": {"_target_": "synth_sod.model_training.loss.FocalLoss", "reduction": "none"}},
+            {"name": "iou_loss", "target_key": "masks", "output_key": "pred_masks", "weight": 1.0,
+             "loss": {"_target_": "synth_sod.model_training.loss.IoULoss", "smooth": 1e-6, "reduction": "none"}},
+            {"name": "mse_ious_loss", "target_key": "gt_ious", "output_key": "pred_iou", "weight": 0.05,
+             "loss": {"_target_": "torch.nn.MSELoss"}},
+        ]
+        lm = LossModule(crit, full_mask_lambda=0.1, decay_rate=0.2)
+        m.train()
+        x = seeded_images(2, 128, 128, seed + 1)
+        masks = ellipse_masks(2, 128, 128, seed + 2)
+        m.zero_grad()
+        o = m(x)
+        loss, parts = lm(o, {"images": x, "masks": masks}, 1)
+        loss.backward()
+        names, norms, slices, nograd = [], [], [], []
+        for n, p in m.named_parameters():
+            if p.grad is None:
+                nograd.append(n)
+                continue
+            names.append(n)
+            norms.append(float(p.grad.norm()))
+            sl = np.full(32, np.nan, np.float32)
+            g = p.grad.reshape(-1)[:32].numpy()
+            sl[:g.size] = g
+            slices.append(sl)
+        bn = {n: b.numpy().copy() for n, b in m.named_buffers() if "running" in n}
+        out.update(train_x=x.numpy(), train_masks=masks.numpy(), rescale=np.float64(rescale), epoch=np.int64(1),
+                   loss=np.float64(loss.item()), parts_names=np.array(sorted(parts)),
+                   parts_values=np.array([float(parts[k]) for k in sorted(parts)]),
+                   train_pred_masks=o["pred_masks"].detach().numpy(),
+                   grad_names=np.array(names), grad_norms=np.array(norms), grad_slices=np.stack(slices),
+                   nograd_names=np.array(nograd),
+                   bn_names=np.array(sorted(bn)), bn_values=np.stack([bn[k] for k in sorted(bn)]))
+        print("dinol train loss", loss.item(), {k: float(v) for k, v in parts.items()}, "no-grad params", len(nograd))
+    finally:
+        D.augment_patches_center_coordinates = orig
+    np.savez_compressed(HERE / "dinol.npz", **out)
+
+
 def main():
     _install_shims()
+    if "--dinol" in sys.argv:
+        torch.set_num_threads(os.cpu_count())
+        gen_dinol()
+        return
     torch.manual_seed(0)
     torch.set_num_threads(os.cpu_count())
     m = build_reference_model(0).eval()

@@ -113,3 +113,49 @@ def test_train_step(synth_sd_torch):
     for n, v in bn.items():
         k = n if n.startswith("seg_head") else n
         assert rel(sd[k].numpy(), v) < 1e-4, n
+
+
+def _dinol_sd():
+    from s3od_amd.weights import synthetic_state_dict
+    return {k: torch.from_numpy(v) for k, v in synthetic_state_dict(0, "dinol", 1).items()}
+
+
+def test_dinol_forward_eval():
+    """dinol (ViT-L/16, taps [4,11,17,23], num_outputs=1) vs the reference built by make_golden.py --dinol."""
+    g = np.load(GOLDEN / "dinol.npz")
+    with torch.no_grad():
+        out = O.forward(torch.from_numpy(g["fwd_x"]), _dinol_sd())
+    assert tuple(out["pred_masks"].shape) == tuple(g["fwd_pred_masks"].shape) == (1, 1, 128, 160)
+    assert rel(out["pred_masks"].numpy(), g["fwd_pred_masks"]) < 1e-4
+    assert rel(out["pred_iou"].numpy(), g["fwd_pred_iou"]) < 1e-4
+    assert rel(out["features"][:, :, ::4, ::4].numpy(), g["fwd_features_sub"]) < 1e-4
+
+
+def test_dinol_train_step_single_mask_loss():
+    """loss.py:166-188 single-mask branch + backward through ViT-L: loss, parts, grad norms / slices,
+    the 32 parameters without gradient (layer 23, final norm, mask_token, refinenet4.resConfUnit1,
+    classifier_head), BN running stats."""
+    g = np.load(GOLDEN / "dinol.npz")
+    sd = _dinol_sd()
+    params = {k: v.requires_grad_(True) for k, v in sd.items() if v.is_floating_point() and "running" not in k}
+    out = O.forward(torch.from_numpy(g["train_x"]), sd, train=True, rope_rescale=float(g["rescale"]))
+    loss, parts = O.single_mask_loss(out, torch.from_numpy(g["train_masks"]))
+    loss.backward()
+    assert abs(loss.item() - float(g["loss"])) < 1e-4 * abs(float(g["loss"]))
+    for n, v in zip(g["parts_names"], g["parts_values"]):
+        assert abs(float(parts[n]) - v) <= 1e-4 * max(abs(v), 1e-6), n
+    for n, nrm, sl in zip(g["grad_names"], g["grad_norms"], g["grad_slices"]):
+        gr = params[n].grad
+        assert gr is not None, n
+        if is_bn_fed_bias(n):
+            continue
+        assert abs(float(gr.norm()) - nrm) <= 1e-3 * max(nrm, 1e-8) + 1e-9, (n, float(gr.norm()), nrm)
+        rms = nrm / np.sqrt(gr.numel())
+        k = np.isfinite(sl)
+        a = np.pad(gr.reshape(-1)[:32].numpy(), (0, 32 - min(32, gr.numel())))[k]
+        assert np.abs(a - sl[k]).max() <= 3e-2 * rms + 1e-12, n
+    nograd = set(g["nograd_names"])
+    assert len(nograd) == 32 and any(".layer.23." in n for n in nograd)
+    assert "seg_head.classifier_head.4.weight" in nograd
+    for n, v in zip(g["bn_names"], g["bn_values"]):
+        assert rel(sd[n].numpy(), v) < 1e-4, n

@@ -13,7 +13,7 @@ tail -5 $OUT/gpu_tests.log
 echo "pytest rc=$rc"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 if [ -z "$NO_BENCH" ]; then
-  timeout -k 10 420 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
+  timeout -k 10 720 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
   brc=$?
   echo "bench rc=$brc"
   tail -c 3000 $OUT/bench.json
