@@ -21,6 +21,7 @@ class _DPTFn(torch.autograd.Function):
         ctx = Ctx()
         out = eng.forward(x, train=True, rope_rescale=rescale, ctx=ctx)
         fctx.s3od = (model, eng, ctx)
+        fctx.set_materialize_grads(False)     # an output the loss never reads arrives as None, not zeros
         fctx.mark_non_differentiable(out["features"])
         return out["pred_masks"], out["pred_iou"], out["features"]
 

@@ -81,6 +81,27 @@ DEV float gelu_erf_grad(float x) {
   return cdf + x * pdf;
 }
 
+// Branch-free erf-GELU for the bf16 path (its output is rounded to bf16, 2^-9 relative): erf by
+// Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7, one v_rcp + one v_exp + 6 FMA and no |x|-range
+// branches (ocml's erff takes several, and they diverge inside a wave).  The f32 strict-parity
+// path keeps erff.  e = exp(-x^2/2) is shared with the derivative: gelu'(x) = Phi(x) + x phi(x).
+DEV void erf_as(float x, float& erf_x, float& e) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float poly = fmaf(t, 1.061405429f, -1.453152027f);
+  poly = fmaf(t, poly, 1.421413741f);
+  poly = fmaf(t, poly, -0.284496736f);
+  poly = fmaf(t, poly, 0.254829592f);
+  poly *= t;
+  e = __expf(-z * z);
+  erf_x = copysignf(fmaf(-poly, e, 1.0f), x);
+}
+DEV float gelu_fast(float x) { float f, e; erf_as(x, f, e); return 0.5f * x * (1.0f + f); }
+DEV float gelu_fast_grad(float x) {
+  float f, e; erf_as(x, f, e);
+  return 0.5f * (1.0f + f) + x * (0.39894228040143268f * e);
+}
+
 // integer dev knob read once from the environment (micro-benchmark sweeps only; default otherwise)
 #include <stdlib.h>
 static inline int dev_knob(const char* name, int def) {

@@ -259,10 +259,10 @@ struct TapWalk {
     if (++tw == TW) { tw = 0; th++; }
     return true;
   }
-  // generic (SC % BK != 0, SC >= BK): advance by BK channels, a tile spans taps tap and tap+1
+  // generic (SC % BK != 0, 2 SC >= BK): advance by BK channels, a tile spans taps tap and tap+1
   DEV void step_any(int kt, int BK, int SC, int TW) {
     if (kt != nk) { int k = kt * BK; tap = k / SC; c0 = k - tap * SC; th = tap / TW; tw = tap - th * TW; }
-    else { c0 += BK; if (c0 >= SC) { c0 -= SC; tap++; if (++tw == TW) { tw = 0; th++; } } }
+    else { c0 += BK; while (c0 >= SC) { c0 -= SC; tap++; if (++tw == TW) { tw = 0; th++; } } }
     nk = kt + 1;
   }
   DEV void next_tap(int TW, int& th1, int& tw1) const { tw1 = tw + 1; th1 = th; if (tw1 == TW) { tw1 = 0; th1++; } }
@@ -280,7 +280,7 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Con
   TapWalk tw;
   HD unsigned long img_bytes() const { return (unsigned long)g.SH * g.SW * g.SC * sizeof(T); }
   HD unsigned long bytes() const { return img_window_bytes(R, g.RH * g.RW, g.B, img_bytes()); }
-  HD bool buf_ok() const { return bytes() < BUF_MAX && g.SC >= BK; }
+  HD bool buf_ok() const { return bytes() < BUF_MAX && 2 * g.SC >= BK; }
   DEV void setup(int t0, int tid) {
     const int lane = tid & 63, wave = wave_id();
     int hw = g.RH * g.RW;
@@ -353,7 +353,7 @@ template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradA {
   TapWalk tw;
   HD unsigned long img_bytes() const { return (unsigned long)g.SH * g.SW * g.SC * sizeof(T); }
   HD unsigned long bytes() const { return img_window_bytes(R, g.RH * g.RW, g.B, img_bytes()); }
-  HD bool buf_ok() const { return bytes() < BUF_MAX && g.SC >= BK; }
+  HD bool buf_ok() const { return bytes() < BUF_MAX && 2 * g.SC >= BK; }
   DEV void setup(int t0, int tid) {
     const int lane = tid & 63, wave = wave_id();
     int hw = g.RH * g.RW;
@@ -424,7 +424,7 @@ template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradB {
   unsigned lo[NIW]; bool cv[NIW]; int kr[NIW];
   TapWalk tw;
   HD unsigned long bytes() const { return (unsigned long)g.SC * g.KH * g.KW * NC * sizeof(T); }
-  HD bool buf_ok() const { return bytes() < BUF_MAX && g.SC >= BK; }
+  HD bool buf_ok() const { return bytes() < BUF_MAX && 2 * g.SC >= BK; }
   DEV void setup(int t0, int tid) {
     const int lane = tid & 63, wave = wave_id();
 #pragma unroll
@@ -846,13 +846,27 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
         for (int e = 0; e < 8; e++) { pv[e] = a[e] + (bias ? bias[n + e] : 0.f); v[e] = pv[e] * (scale ? scale[n + e] : 1.f) + (shift ? shift[n + e] : 0.f); }
       }
       if (pre) store8<TP>(pre + orow * ldp + n, pv);
-      if (act >= ACT_GELU_BWD) {
+      // act is uniform: branch once per segment, so the erf path is never speculated for the others
+      constexpr bool FAST = sizeof(TP) == 2;     // bf16 compute: branch-free GELU (common.hpp)
+      if (act == ACT_GELU_BWD) {
         float r[8]; load8<TR>(res1 + orow * ldr1 + n, r);
 #pragma unroll
-        for (int e = 0; e < 8; e++) o[e] = act == ACT_GELU_BWD ? v[e] * gelu_erf_grad(r[e]) : (r[e] > 0.f ? v[e] : 0.f);
-      } else {
+        for (int e = 0; e < 8; e++) o[e] = v[e] * (FAST ? gelu_fast_grad(r[e]) : gelu_erf_grad(r[e]));
+      } else if (act == ACT_RELU_BWD) {
+        float r[8]; load8<TR>(res1 + orow * ldr1 + n, r);
 #pragma unroll
-        for (int e = 0; e < 8; e++) o[e] = act == ACT_RELU ? fmaxf(v[e], 0.f) : (act == ACT_GELU ? gelu_erf(v[e]) : v[e]);
+        for (int e = 0; e < 8; e++) o[e] = r[e] > 0.f ? v[e] : 0.f;
+      } else {
+        if (act == ACT_GELU) {
+#pragma unroll
+          for (int e = 0; e < 8; e++) o[e] = FAST ? gelu_fast(v[e]) : gelu_erf(v[e]);
+        } else if (act == ACT_RELU) {
+#pragma unroll
+          for (int e = 0; e < 8; e++) o[e] = fmaxf(v[e], 0.f);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; e++) o[e] = v[e];
+        }
         if (res1) { float r[8]; load8<TR>(res1 + orow * ldr1 + n, r);
 #pragma unroll
           for (int e = 0; e < 8; e++) o[e] += r[e]; }
@@ -923,7 +937,7 @@ struct EpiWgrad {
 template <typename T, int BM, int BN, class LA, class LB, class EPI, int NST = 3, int WM_ = 0>
 static int launch_igemm(LA la, LB lb, EPI epi, int M, int N, int KTILES, int split, int zdim_extra, hipStream_t st) {
   if (!la.buf_ok() || !lb.buf_ok()) {
-    s3od_set_error("igemm: operand too large for a buffer descriptor or gather channels < %d", KT<T>::BK);
+    s3od_set_error("igemm: operand window too large for a buffer descriptor or gather channels < %d", KT<T>::BK / 2);
     return 22;
   }
   {

@@ -233,7 +233,10 @@ int s3od_linear_wgrad(int dtype, int Nout, int Kin, int rows, const void* dy, lo
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(rows, KT<T>::BK);
-    return with_cfg<T>(4, [&](auto C) -> int {
+    // measured (tools/lin_sweep.py, bs16 1024^2 ViT shapes): 128x128 tiles for the large outputs
+    // (3072x768, 2304x768, 768x3072: 7-12 % faster than 256x256), 256x128 for 768x768
+    const int def = (long)Nout * Kin <= 1024L * 1024 ? 0 : 1;
+    return with_cfg<T>(def, [&](auto C) -> int {
       constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
       int sp = split > 0 ? split : wgrad_split<T, BM, BN, NST>(cdiv(Nout, BM) * cdiv(Kin, BN), KTILES);
       DenseMC<T, BM, decltype(C)::W> la{(const T*)dy, lddy, rows, Nout};

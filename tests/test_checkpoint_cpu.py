@@ -66,3 +66,22 @@ def test_export_clean_checkpoint(tmp_path):
     assert set(clean["state_dict"]) == set(m.state_dict())
     m2 = DPTSegmentation()
     m2.load_state_dict(clean["state_dict"])
+
+
+def test_export_model_cli(tmp_path):
+    """scripts/export_model.py (reference scripts/export_model.py:175-227): --checkpoint/--output/--format."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    m = DPTSegmentation(init_seed=None)
+    save_checkpoint(tmp_path / "best.ckpt", m, config={"model": {"_target_": "synth_sod.model_training.model.DPTSegmentation"}})
+    script = Path(__file__).resolve().parent.parent / "scripts" / "export_model.py"
+    r = subprocess.run([sys.executable, str(script), "--checkpoint", str(tmp_path / "best.ckpt"), "--output",
+                        str(tmp_path / "s3od.pt")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "contains 371 parameters" in r.stdout
+    clean = torch.load(tmp_path / "s3od.pt", map_location="cpu", weights_only=True)
+    assert set(clean["state_dict"]) == set(m.state_dict())
+    r = subprocess.run([sys.executable, str(script), "--checkpoint", str(tmp_path / "best.ckpt"), "--output",
+                        str(tmp_path / "x.pt"), "--format", "torchscript"], capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "TorchScript" in r.stderr

@@ -1,0 +1,91 @@
+"""Time the ViT linear GEMMs of the bs=16 1024^2 training step with their REAL epilogues, through the
+C ABI, for the tile config selected by S3OD_GEMM_CFG (dev tool; run once per config).
+
+    S3OD_GEMM_CFG=4 python tools/lin_sweep.py
+"""
+import os
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+from s3od_amd._lib import lib, stream, BF16  # noqa: E402
+
+M, D, F = 65616, 768, 3072
+ACT_GELU, ACT_GELU_BWD = 2, 3
+
+
+def timeit(fn, n=10):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n * 1e-3
+
+
+def r(*s, dt=torch.bfloat16):
+    return torch.randn(*s, device="cuda").to(dt)
+
+
+def fwd(name, N, K, act=0, res_f32=False, out_f32=False, pre=False, scale=False):
+    x, w, b = r(M, K), r(N, K), r(N, dt=torch.float32)
+    out = torch.empty(M, N, device="cuda", dtype=torch.float32 if out_f32 else torch.bfloat16)
+    res = r(M, N, dt=torch.float32) if res_f32 else None
+    pr = torch.empty(M, N, device="cuda", dtype=torch.bfloat16) if pre else None
+    sc = r(N, dt=torch.float32) if scale else None
+    f = lambda: lib()("s3od_linear_fwd", BF16, M, N, K, x, K, w, b, sc, None, act, res, N, None, 0, int(res_f32), out, N,
+                      int(out_f32), pr, N, 0, 0, 0, stream())
+    report(name, 2.0 * M * N * K, timeit(f))
+
+
+def dgrad(name, N, K, act=0, out_f32=False, aux=False):
+    dy, w = r(M, K), r(K, N)
+    out = torch.empty(M, N, device="cuda", dtype=torch.float32 if out_f32 else torch.bfloat16)
+    ax = r(M, N) if aux else None
+    f = lambda: lib()("s3od_linear_dgrad", BF16, M, N, K, dy, K, w, act, ax, N, out, N, int(out_f32), 0, 0, 0, None, stream())
+    report(name, 2.0 * M * N * K, timeit(f))
+
+
+def wgrad(name, Nout, Kin):
+    dy, x = r(M, Nout), r(M, Kin)
+    dw = torch.zeros(Nout, Kin, device="cuda")
+    f = lambda: lib()("s3od_linear_wgrad", BF16, Nout, Kin, M, dy, Nout, x, Kin, dw, 0, stream())
+    report(name, 2.0 * M * Nout * Kin, timeit(f))
+
+
+def qkv():
+    B, Nt, P = 16, 4101, 4096
+    x, w, b = r(B * Nt, D), r(3 * D, D), r(3 * D, dt=torch.float32)
+    cs, sn = r(P, 64, dt=torch.float32), r(P, 64, dt=torch.float32)
+    q, k, v = (torch.empty(B * 12, Nt, 64, device="cuda", dtype=torch.bfloat16) for _ in range(3))
+    f = lambda: lib()("s3od_qkv_rope_fwd", BF16, B, Nt, P, 12, x, w, b, cs, sn, q, k, v, stream())
+    report("qkv_rope fwd N2304 K768", 2.0 * B * Nt * 3 * D * D, timeit(f))
+
+
+def report(name, fl, t):
+    print(f"cfg {os.environ.get('S3OD_GEMM_CFG', 'def'):>3}  {name:40s} {t * 1e6:8.1f} us {fl / t / 1e12:7.1f} TF/s", flush=True)
+
+
+if __name__ == "__main__":
+    qkv()
+    fwd("o_proj fwd N768 K768 (res f32, out f32, pre)", D, D, res_f32=True, out_f32=True, pre=True, scale=True)
+    fwd("up fwd N3072 K768 (GELU, pre)", F, D, act=ACT_GELU, pre=True)
+    fwd("down fwd N768 K3072 (res f32, out f32, pre)", D, F, res_f32=True, out_f32=True, pre=True, scale=True)
+    dgrad("down dgrad N3072 K768 (GELU')", F, D, act=ACT_GELU_BWD, aux=True)
+    dgrad("up dgrad N768 K3072", D, F)
+    dgrad("qkv dgrad N768 K2304", D, 3 * D)
+    dgrad("o dgrad N768 K768", D, D)
+    wgrad("wgrad 3072x768", F, D)
+    wgrad("wgrad 768x3072", D, F)
+    wgrad("wgrad 2304x768", 3 * D, D)
+    wgrad("wgrad 768x768", D, D)
+    # hipBLASLt yardstick (not used by the product): plain bf16 matmul, bf16 out
+    for (N, K) in ((F, D), (D, F), (3 * D, D), (D, D)):
+        a, bb = r(M, K), r(K, N)
+        report(f"hipBLASLt torch.matmul N{N} K{K}", 2.0 * M * N * K, timeit(lambda: torch.matmul(a, bb)))

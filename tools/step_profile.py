@@ -29,8 +29,9 @@ def flops(name, a):
         N, K, R = a[1:4]
         return 2.0 * N * K * R, f"N{N} K{K} rows{R}"
     if name == "s3od_qkv_rope_fwd":
-        B, Nt = a[1:3]
-        return 2.0 * B * Nt * 2304 * 768, f"B{B} Nt{Nt}"
+        B, Nt, P, H = a[1:5]
+        D = 64 * H
+        return 2.0 * B * Nt * 3 * D * D, f"B{B} Nt{Nt} D{D}"
     if name in ("s3od_conv_fwd", "s3od_conv_dgrad", "s3od_conv_wgrad"):
         B, H, W, Cin, OH, OW, Cout, KH, KW, s, p = a[1:12]
         if name == "s3od_conv_dgrad" and s > 1 and OH > H:   # ConvT forward: Y-grid is the big one
