@@ -68,8 +68,16 @@ def qkv():
     report("qkv_rope fwd N2304 K768", 2.0 * B * Nt * 3 * D * D, timeit(f))
 
 
+def conv(name, B, H, Cin, Cout, k=3, act=0):
+    x, w, b = r(B, H, H, Cin), r(Cout, k, k, Cin), r(Cout, dt=torch.float32)
+    out = torch.empty(B, H, H, Cout, device="cuda", dtype=torch.bfloat16)
+    f = lambda: lib()("s3od_conv_fwd", BF16, B, H, H, Cin, H, H, Cout, k, k, 1, k // 2, x, 0, w, b, None, None, act, None, None,
+                      out, None, None, None, stream())
+    report(name, 2.0 * B * H * H * Cout * Cin * k * k, timeit(f))
+
+
 def report(name, fl, t):
-    print(f"cfg {os.environ.get('S3OD_GEMM_CFG', 'def'):>3}  {name:40s} {t * 1e6:8.1f} us {fl / t / 1e12:7.1f} TF/s", flush=True)
+    print(f"cfg {os.environ.get('S3OD_GEMM_CFG', 'def'):>3} {name:40s} {t * 1e6:8.1f} us {fl / t / 1e12:7.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
@@ -85,6 +93,9 @@ if __name__ == "__main__":
     wgrad("wgrad 768x3072", D, F)
     wgrad("wgrad 2304x768", 3 * D, D)
     wgrad("wgrad 768x768", D, D)
+    conv("conv fwd 256->256 3x3 @256^2 bs16", 16, 256, 256, 256)
+    conv("conv fwd 64->64 3x3 @1024^2 bs16 relu", 16, 1024, 64, 64, act=1)
+    conv("conv fwd 256->128 3x3 @512^2 bs16", 16, 512, 256, 128)
     # hipBLASLt yardstick (not used by the product): plain bf16 matmul, bf16 out
     for (N, K) in ((F, D), (D, F), (3 * D, D), (D, D)):
         a, bb = r(M, K), r(K, N)
