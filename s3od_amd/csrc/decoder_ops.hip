@@ -23,6 +23,25 @@ __global__ void repack_kernel(const float* __restrict__ src, T* __restrict__ dst
   dst[idx] = from_f<T>(src[((long)o * I + i) * KHW + t]);
 }
 
+// Multi-tensor form: every packed weight of the model in ONE launch (the fp32 masters change after
+// each optimizer step, so the whole set is re-packed per step).  tab: device int64 [T][6] =
+// {src ptr, dst ptr, O, I, KH*KW, dst element offset}; chunk_t / chunk_o map blocks -> (tensor, start).
+template <typename T>
+__global__ void __launch_bounds__(256) repack_multi_kernel(const long* __restrict__ tab, const int* __restrict__ chunk_t,
+                                                           const long* __restrict__ chunk_o, int chunk) {
+  const int t = chunk_t[blockIdx.x];
+  const long o0 = chunk_o[blockIdx.x];
+  const float* src = (const float*)tab[6 * t + 0];
+  T* dst = (T*)tab[6 * t + 1] + tab[6 * t + 5];
+  const int O = (int)tab[6 * t + 2], I = (int)tab[6 * t + 3], KHW = (int)tab[6 * t + 4];
+  const long total = (long)O * I * KHW;
+  const long o1 = min(total, o0 + chunk);
+  for (long idx = o0 + threadIdx.x; idx < o1; idx += blockDim.x) {
+    int i = idx % I; long r = idx / I; int tp = r % KHW; int o = r / KHW;
+    dst[idx] = from_f<T>(src[((long)o * I + i) * KHW + tp]);
+  }
+}
+
 // ConvTranspose2d weight [Cin_T][Cout_T][KH][KW] IS the conv-view weight [cout_c][cin_c][KH][KW]; no flip.
 
 // ---------------------------------------------------------------- BatchNorm
@@ -330,27 +349,24 @@ __global__ void iou_head_fwd_kernel(const float* pooled, const float* w1, const 
 }
 
 // backward of the head: given dout [B,NM] -> dw2, db2, dw1, db1 (accumulate) and dpooled/HW [B,256] (bcast for p1)
+// one block of 256 threads per image (fp32 atomics into the shared weight gradients)
 __global__ void iou_head_bwd_kernel(const float* pooled, const float* hid, const float* w1, const float* w2, const float* dout,
                                     float* dw1, float* db1, float* dw2, float* db2, float* dpix, int B, float inv_hw, int NM) {
-  // single block of 256 threads; B is small
   __shared__ float dh[64];
-  int t = threadIdx.x;
-  for (int b = 0; b < B; b++) {
-    const float* d = dout + b * NM;
-    if (t < 64) {
-      float g = 0.f;
-      for (int j = 0; j < NM; j++) { g += d[j] * w2[j * 64 + t]; atomicAdd(dw2 + j * 64 + t, d[j] * hid[b * 64 + t]); }
-      dh[t] = hid[b * 64 + t] > 0.f ? g : 0.f;
-      atomicAdd(db1 + t, dh[t]);
-    }
-    if (t < NM) atomicAdd(db2 + t, d[t]);
-    __syncthreads();
-    // dw1[j][k] += dh[j]*pooled[k];  dpooled[k] = sum_j dh[j] w1[j][k]
-    float dp = 0.f;
-    for (int j = 0; j < 64; j++) { atomicAdd(dw1 + j * 256 + t, dh[j] * pooled[b * 256 + t]); dp += dh[j] * w1[j * 256 + t]; }
-    dpix[b * 256 + t] = dp * inv_hw;
-    __syncthreads();
+  const int t = threadIdx.x, b = blockIdx.x;
+  const float* d = dout + b * NM;
+  if (t < 64) {
+    float g = 0.f;
+    for (int j = 0; j < NM; j++) { g += d[j] * w2[j * 64 + t]; atomicAdd(dw2 + j * 64 + t, d[j] * hid[b * 64 + t]); }
+    dh[t] = hid[b * 64 + t] > 0.f ? g : 0.f;
+    atomicAdd(db1 + t, dh[t]);
   }
+  if (t < NM) atomicAdd(db2 + t, d[t]);
+  __syncthreads();
+  // dw1[j][k] += dh[j]*pooled[k];  dpooled[k] = sum_j dh[j] w1[j][k]
+  float dp = 0.f;
+  for (int j = 0; j < 64; j++) { atomicAdd(dw1 + j * 256 + t, dh[j] * pooled[b * 256 + t]); dp += dh[j] * w1[j * 256 + t]; }
+  dpix[b * 256 + t] = dp * inv_hw;
 }
 
 // ---------------------------------------------------------------- mask-head backward prologue
@@ -416,6 +432,17 @@ int s3od_repack_weight(int dtype, const float* src, void* dst, int O, int I, int
     hipLaunchKernelGGL(repack_kernel<T>, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream, src, (T*)dst, O, I, KH * KW);
   });
   return s3od_check_launch("repack_weight");
+}
+
+// tab: device int64 [ntensors][6] (src f32*, dst T* (or f32* for dtype F32 / fp32 biases), O, I, KH*KW,
+// dst element offset); chunk_t / chunk_o: device table of nchunks blocks (chunk elements each)
+int s3od_repack_multi(int dtype, const long* tab, const int* chunk_t, const long* chunk_o, int nchunks, int chunk, void* stream) {
+  S3OD_REQUIRE(nchunks >= 0 && chunk > 0, "repack_multi: bad chunk table");
+  if (nchunks == 0) return 0;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL(repack_multi_kernel<T>, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, tab, chunk_t, chunk_o, chunk);
+  });
+  return s3od_check_launch("repack_multi");
 }
 
 int s3od_bn_fold(const float* w, const float* b, const float* rm, const float* rv, float eps,
@@ -507,7 +534,7 @@ int s3od_iou_head_fwd(const float* pooled, const float* w1, const float* b1, con
 int s3od_iou_head_bwd(const float* pooled, const float* hid, const float* w1, const float* w2, const float* dout, float* dw1,
                       float* db1, float* dw2, float* db2, float* dpix, int B, int HW, int NM, void* stream) {
   S3OD_REQUIRE(NM >= 1 && NM <= 64, "iou_head_bwd: %d outputs", NM);
-  hipLaunchKernelGGL(iou_head_bwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, pooled, hid, w1, w2, dout, dw1, db1, dw2, db2,
+  hipLaunchKernelGGL(iou_head_bwd_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, pooled, hid, w1, w2, dout, dw1, db1, dw2, db2,
                      dpix, B, 1.0f / (float)HW, NM);
   return s3od_check_launch("iou_head_bwd");
 }

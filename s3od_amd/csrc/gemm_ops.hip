@@ -183,7 +183,7 @@ int s3od_linear_fwd(int dtype, int M, int N, int K, const void* x, long ldx, con
       typedef decltype(tout) TO; typedef decltype(tres) TR;
       // measured (tools/lin_sweep.py): 256x128 x 3 stages for K >= 2048; the GELU(+pre) up-projection
       // runs best on 256x256 tiles (574 vs 621 us at M=65616 N=3072 K=768); 128x128 otherwise
-      const int def = K >= 2048 ? 0 : (act == 2 /*ACT_GELU*/ && N >= 2048 ? 4 : 1);
+      const int def = K >= 2048 ? 0 : (act == ACT_GELU && N >= 2048 ? 4 : 1);
       return with_cfg<T>(def, [&](auto C) -> int {
         constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
         DenseKC<T, BM, decltype(C)::W> la{(const T*)x, ldx, M, K, 0};

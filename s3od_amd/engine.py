@@ -59,40 +59,61 @@ class DPTEngine:
         self.dt = BF16 if compute_dtype == "bf16" else F32
         self.tdt = torch.bfloat16 if compute_dtype == "bf16" else torch.float32
         self._wkey = None
+        self._packs = None
 
     # ------------------------------------------------------------------ weights
     def _version_key(self):
         return (self.cdt, sum(int(v._version) for v in self.p.values()), id(self))
 
     def prepare(self, force=False):
-        """Repack / cast all fp32 parameters into kernel layouts (cached until params change)."""
+        """Repack / cast all fp32 parameters into kernel layouts (cached until params change).
+
+        The packed buffers are allocated once; every refresh (after each optimizer step) is two
+        launches of ``s3od_repack_multi`` -- one for the compute-dtype weights, one for the fp32
+        fused bias vectors -- instead of ~100 per-tensor repacks and torch copies."""
         key = self._version_key()
         if not force and key == self._wkey:
             return
-        L, P, dt, T = lib(), self.p, self.dt, self.tdt
-        st = stream()
-        dev = next(iter(P.values())).device
-        w = {}
+        ptrs = tuple(v.data_ptr() for v in self.p.values())
+        if getattr(self, "_packs", None) is None or self._packs["ptrs"] != ptrs or self._packs["dt"] != self.dt:
+            self._build_packs(ptrs)
+        L, st = lib(), stream()
         L.phase = "prepare"
+        for dt, tab in self._packs["tabs"]:
+            L("s3od_repack_multi", dt, tab["tab"], tab["ct"], tab["co"], tab["n"], self._REPACK_CHUNK, st)
+        L.phase = None
+        self._wkey = key
 
-        def pack(name, O, I, KH=1, KW=1, out=None):
-            out = torch.empty((O, KH, KW, I), dtype=T, device=dev) if out is None else out
-            L("s3od_repack_weight", dt, P[name], out, O, I, KH, KW, st)
-            return out
+    _REPACK_CHUNK = 16384
+
+    def _build_packs(self, ptrs):
+        """Allocate the kernel-layout buffers and the device tables that fill them from the masters."""
+        P, T = self.p, self.tdt
+        dev = next(iter(P.values())).device
+        D, MLP, nm = self.D, self.MLP, self.nm
+        ents = {self.dt: [], F32: []}          # dtype -> [(src, dst, dst_offset, O, I, KHW)]
+        w = {}
+
+        def pack(name, O, I, KH=1, KW=1, dst=None, off=0):
+            if dst is None:
+                dst = torch.empty((O, KH, KW, I), dtype=T, device=dev)
+            ents[self.dt].append((P[name], dst, off, O, I, KH * KW))
+            return dst
+
+        def copy32(name, dst, off, n):
+            ents[F32].append((P[name], dst, off, n, 1, 1))
 
         e = "encoder.embeddings."
-        D, MLP, nm = self.D, self.MLP, self.nm
         w["pe"] = pack(e + "patch_embeddings.weight", D, 3 * 16 * 16)
         for i in range(self.last):
             p = f"encoder.model.layer.{i}."
             qkv = torch.empty((3 * D, D), dtype=T, device=dev)
-            pack(p + "attention.q_proj.weight", D, D, out=qkv[0:D])
-            pack(p + "attention.k_proj.weight", D, D, out=qkv[D:2 * D])
-            pack(p + "attention.v_proj.weight", D, D, out=qkv[2 * D:])
+            for j, nme in enumerate(("q_proj", "k_proj", "v_proj")):
+                pack(p + f"attention.{nme}.weight", D, D, dst=qkv, off=j * D * D)
             w[f"qkv{i}"] = qkv
-            bq = torch.zeros(3 * D, dtype=torch.float32, device=dev)
-            bq[:D].copy_(P[p + "attention.q_proj.bias"])
-            bq[2 * D:].copy_(P[p + "attention.v_proj.bias"])
+            bq = torch.zeros(3 * D, dtype=torch.float32, device=dev)      # k_proj has no bias (key_bias=False)
+            copy32(p + "attention.q_proj.bias", bq, 0, D)
+            copy32(p + "attention.v_proj.bias", bq, 2 * D, D)
             w[f"bqkv{i}"] = bq
             w[f"o{i}"] = pack(p + "attention.o_proj.weight", D, D)
             w[f"up{i}"] = pack(p + "mlp.up_proj.weight", MLP, D)
@@ -117,14 +138,24 @@ class DPTEngine:
         w["c64"] = pack(m + "upsample_2x.2.weight", 64, 64, 3, 3)
         heads = torch.empty((32 * nm, 3, 3, 64), dtype=T, device=dev)
         for k in range(nm):
-            pack(m + f"mask_heads.{k}.0.weight", 32, 64, 3, 3, out=heads[32 * k:32 * (k + 1)])
+            pack(m + f"mask_heads.{k}.0.weight", 32, 64, 3, 3, dst=heads, off=k * 32 * 9 * 64)
         w["heads1"] = heads
-        w["heads1_b"] = torch.cat([P[m + f"mask_heads.{k}.0.bias"] for k in range(nm)])
-        w["heads2"] = torch.cat([P[m + f"mask_heads.{k}.2.weight"].reshape(32) for k in range(nm)])
-        w["heads2_b"] = torch.cat([P[m + f"mask_heads.{k}.2.bias"] for k in range(nm)])
+        for key, n, per in (("heads1_b", "0.bias", 32), ("heads2", "2.weight", 32), ("heads2_b", "2.bias", 1)):
+            w[key] = torch.empty(per * nm, dtype=torch.float32, device=dev)
+            for k in range(nm):
+                copy32(m + f"mask_heads.{k}.{n}", w[key], k * per, per)
+        tabs = []
+        for dt, lst in ents.items():
+            rows, ct, co = [], [], []
+            for t, (src, dst, off, O, I, KHW) in enumerate(lst):
+                rows.append([src.data_ptr(), dst.data_ptr(), O, I, KHW, off])
+                for o in range(0, O * I * KHW, self._REPACK_CHUNK):
+                    ct.append(t); co.append(o)
+            tabs.append((dt, dict(tab=torch.tensor(rows, dtype=torch.int64, device=dev),
+                                  ct=torch.tensor(ct, dtype=torch.int32, device=dev),
+                                  co=torch.tensor(co, dtype=torch.int64, device=dev), n=len(ct))))
         self.w = w
-        self._wkey = key
-        L.phase = None
+        self._packs = {"ptrs": ptrs, "dt": self.dt, "tabs": tabs}
 
     # ------------------------------------------------------------------ helpers
     def _lin(self, x, w, M, N, K, out, bias=None, scale=None, shift=None, act=ACT_NONE, res1=None, res_f32=False,

@@ -30,6 +30,7 @@ REF = {
     "s3od_layerscale_bwd": "DINOv3ViTLayerScale backward: tf:modeling_dinov3_vit.py:337-343",
     "s3od_qkv_unrope": "apply_rotary_pos_emb backward: tf:modeling_dinov3_vit.py:238-268",
     "s3od_repack_weight": "weight layout for the kernels (the reference's state_dict layout is kept for params)",
+    "s3od_repack_multi": "all kernel-layout weight repacks of one optimizer step in one launch (reference: none; PyTorch reads its fp32 parameters directly)",
     "s3od_bn_fold": "nn.BatchNorm2d eval-mode affine: src/s3od/model.py:326-343",
     "s3od_bn_finalize": "nn.BatchNorm2d train-mode batch statistics + running-stat update (momentum 0.1)",
     "s3od_affine_act": "BatchNorm apply + ReLU + residual: src/s3od/model.py:334-345, 383-393",
