@@ -93,3 +93,82 @@ def test_regular_mode_reproducible_and_sane():
     hi = torch.tensor(((1 - MEAN) / STD), dtype=torch.float32).view(1, 3, 1, 1).cuda()
     assert (a["images"] >= lo - 1e-5).all() and (a["images"] <= hi + 1e-5).all()
     assert set(torch.unique(a["masks"]).tolist()) <= {0.0, 1.0}
+
+
+def _denorm(t):
+    return t.cpu().numpy() * STD[:, None, None] + MEAN[:, None, None]
+
+
+def test_synthetic_identity_chain_equals_test_mode():
+    """raw geometry pass + the synthetic photometric passes with every effect at identity == the
+    test-mode (letterbox + Normalize) output: the plumbing of the three-pass pipeline is exact."""
+    from s3od_amd.data import GpuAugment, SynthParams
+    from s3od_amd._lib import lib, stream
+    S = 96
+    smp = _sample(80, 120, 4)
+    base = GpuAugment(S, mode="test")([smp])
+    aug = GpuAugment(S, mode="test")
+    p = aug.sample_params(80, 120, smp["image"])
+    p.raw = 1
+    img = torch.from_numpy(smp["image"]).cuda(); msk = torch.from_numpy(smp["mask"]).cuda()
+    raw = torch.empty(3, S, S, device="cuda"); om = torch.empty(S, S, device="cuda"); out = torch.empty(3, S, S, device="cuda")
+    lib()("s3od_augment_sample", img, msk, ctypes.addressof(p), S, raw, om, stream())
+    q = SynthParams.identity()
+    lib()("s3od_augment_synthetic", raw, ctypes.addressof(q), None, S, out, stream())
+    torch.cuda.synchronize()
+    assert float((out - base["images"][0]).abs().max()) < 1e-5
+    assert torch.equal(om, base["masks"][0])
+
+
+@pytest.mark.parametrize("what", ["gray", "posterize", "blur_const", "shuffle"])
+def test_synthetic_effects_exact_properties(what):
+    from s3od_amd.data import SynthParams
+    from s3od_amd._lib import lib, stream
+    S = 64
+    g = torch.Generator(device="cuda").manual_seed(1)
+    raw = torch.rand(3, S, S, device="cuda", generator=g)
+    if what == "blur_const":
+        raw = torch.full((3, S, S), 0.3, device="cuda")
+    ref = raw.clone()
+    q = SynthParams.identity()
+    kw = None
+    if what == "gray":
+        q.color_op = 2
+    elif what == "posterize":
+        q.post_bits = 5
+    elif what == "blur_const":
+        q.ksize = 5
+        kw = torch.full((25,), 1 / 25, device="cuda")
+    elif what == "shuffle":
+        q.color_op = 3
+        q.perm[0], q.perm[1], q.perm[2] = 2, 0, 1
+    out = torch.empty(3, S, S, device="cuda")
+    lib()("s3od_augment_synthetic", raw, ctypes.addressof(q), kw, S, out, stream())
+    torch.cuda.synchronize()
+    v = _denorm(out)
+    r = ref.cpu().numpy()
+    if what == "gray":
+        assert np.abs(v[0] - v[1]).max() < 1e-5 and np.abs(v[1] - v[2]).max() < 1e-5
+        assert np.abs(v[0] - (0.299 * r[0] + 0.587 * r[1] + 0.114 * r[2])).max() < 1e-5
+    elif what == "posterize":
+        q8 = np.round(v * 255)
+        assert np.abs(v * 255 - q8).max() < 1e-3 and (q8.astype(int) % 8 == 0).all()
+    elif what == "blur_const":
+        assert np.abs(v - 0.3).max() < 1e-5
+    elif what == "shuffle":
+        assert np.abs(v - r[[2, 0, 1]]).max() < 1e-5
+
+
+def test_synthetic_mode_reproducible_and_sane():
+    from s3od_amd.data import GpuAugment
+    smps = [_sample(120 + 7 * i, 90 + 11 * i, i) for i in range(8)]
+    a = GpuAugment(96, mode="synthetic", seed=9)(smps)
+    b = GpuAugment(96, mode="synthetic", seed=9)(smps)
+    torch.cuda.synchronize()
+    assert torch.equal(a["images"], b["images"]) and torch.equal(a["masks"], b["masks"])
+    lo = torch.tensor(((0 - MEAN) / STD), dtype=torch.float32).view(1, 3, 1, 1).cuda()
+    hi = torch.tensor(((1 - MEAN) / STD), dtype=torch.float32).view(1, 3, 1, 1).cuda()
+    assert torch.isfinite(a["images"]).all()
+    assert (a["images"] >= lo - 1e-5).all() and (a["images"] <= hi + 1e-5).all()
+    assert set(torch.unique(a["masks"]).tolist()) <= {0.0, 1.0}
+    assert a["masks"].sum() > 0
