@@ -159,6 +159,8 @@ def breakdown(step, steps, peak):
         for key, tab in ((name, by_entry), (klass(name), by_class)):
             d = tab.setdefault(key, {"ms": 0.0, "calls": 0, "kind": kind, "work": 0.0})
             d["ms"] += ms; d["calls"] += 1; d["work"] += work
+            if kind != "other" and d["kind"] == "other":
+                d["kind"] = kind
     tot = sum(d["ms"] for d in by_entry.values())
 
     def fmt(d):

@@ -7,7 +7,7 @@
 # Each step has its own time limit; steps are chained with && (nothing runs after a failure).
 # usage: bash tools/profile_round.sh <tag> [roofline-kernel-regex]
 TAG=${1:-r02}
-KRE=${2:-attn_bwd_dkdv_kernel}
+KRE=${2:-attn_(bwd|delta)}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
