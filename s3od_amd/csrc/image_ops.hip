@@ -122,15 +122,16 @@ int s3od_preprocess(const void* img, int H0, int W0, int new_h, int new_w, int p
   return s3od_check_launch("preprocess");
 }
 
-// logits: fp32 [3][LH][LW] (one image; LH x LW = S x S, or S x 16*floor(new_w/16) for the
-// reference's unpadded Quirk-2 input); tmp: fp32 [3][h][W0]; out: fp32 [3][H0][W0]
-int s3od_sigmoid_unpad_resize(const float* logits, int LH, int LW, int pad_h, int pad_w, int h, int w, int H0, int W0,
+// logits: fp32 [NM][LH][LW] (one image, NM masks; LH x LW = S x S, or S x 16*floor(new_w/16) for the
+// reference's unpadded Quirk-2 input); tmp: fp32 [NM][h][W0]; out: fp32 [NM][H0][W0]
+int s3od_sigmoid_unpad_resize(const float* logits, int NM, int LH, int LW, int pad_h, int pad_w, int h, int w, int H0, int W0,
                               float* tmp, float* out, void* stream) {
+  S3OD_REQUIRE(NM >= 1 && NM <= 64 && h > 0 && w > 0, "postprocess: bad mask count / crop");
   S3OD_REQUIRE((float)w / W0 < 32.f && (float)h / H0 < 32.f, "postprocess: downscale factor too large");
   S3OD_REQUIRE(pad_h + h <= LH && pad_w + w <= LW, "postprocess: crop outside the logits");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(post_h_kernel, dim3(cdiv(W0, 256), h, 3), dim3(256), 0, st, logits, LH, LW, pad_h, pad_w, h, w, W0, tmp);
-  hipLaunchKernelGGL(post_v_kernel, dim3(cdiv(W0, 256), H0, 3), dim3(256), 0, st, tmp, h, H0, W0, out);
+  hipLaunchKernelGGL(post_h_kernel, dim3(cdiv(W0, 256), h, NM), dim3(256), 0, st, logits, LH, LW, pad_h, pad_w, h, w, W0, tmp);
+  hipLaunchKernelGGL(post_v_kernel, dim3(cdiv(W0, 256), H0, NM), dim3(256), 0, st, tmp, h, H0, W0, out);
   return s3od_check_launch("sigmoid_unpad_resize");
 }
 

@@ -122,9 +122,10 @@ class BackgroundRemoval:
         H0, W0 = pad["original_size"]
         LH, LW = out["pred_masks"].shape[2], out["pred_masks"].shape[3]
         h, w = LH - 2 * pad["height_pad"], LW - 2 * pad["width_pad"]
-        tmp = torch.empty((3, h, W0), dtype=torch.float32, device=x.device)
-        masks = torch.empty((3, H0, W0), dtype=torch.float32, device=x.device)
-        lib()("s3od_sigmoid_unpad_resize", out["pred_masks"].contiguous(), LH, LW, pad["height_pad"], pad["width_pad"], h, w,
+        NM = out["pred_masks"].shape[1]
+        tmp = torch.empty((NM, h, W0), dtype=torch.float32, device=x.device)
+        masks = torch.empty((NM, H0, W0), dtype=torch.float32, device=x.device)
+        lib()("s3od_sigmoid_unpad_resize", out["pred_masks"].contiguous(), NM, LH, LW, pad["height_pad"], pad["width_pad"], h, w,
               H0, W0, tmp, masks, stream())
         pred_ious = torch.sigmoid(out["pred_iou"]).squeeze(0).cpu().numpy()   # 3 floats
         all_masks = masks.cpu().numpy()

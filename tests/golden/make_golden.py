@@ -292,8 +292,77 @@ def gen_dinol(seed=7, rescale=0.83):
     np.savez_compressed(HERE / "dinol.npz", **out)
 
 
+def metric_cases(seed=11):
+    """(name, pred float32 [H,W] in [0,1], gt float64 {0,1}) pairs covering the metric edge cases."""
+    r = np.random.default_rng(seed)
+
+    def ell(H, W, cy, cx, ry, rx):
+        yy, xx = np.mgrid[:H, :W]
+        return ((yy - cy) ** 2 / ry ** 2 + (xx - cx) ** 2 / rx ** 2) < 1
+
+    def smooth(H, W):
+        from scipy.ndimage import gaussian_filter
+        f = gaussian_filter(r.standard_normal((H, W)), 4)
+        return (1 / (1 + np.exp(-6 * f / f.std()))).astype(np.float32)
+
+    cases = []
+    g = ell(48, 64, 20, 30, 12, 18)
+    cases.append(("random_48x64", r.random((48, 64)).astype(np.float32), g))
+    g = ell(97, 131, 50, 60, 30, 45) & ~ell(97, 131, 50, 60, 8, 10)
+    p = np.clip(0.7 * g + 0.3 * smooth(97, 131), 0, 1).astype(np.float32)
+    cases.append(("holes_97x131", p, g))
+    cases.append(("empty_gt_160x120", r.random((160, 120)).astype(np.float32), np.zeros((160, 120), bool)))
+    cases.append(("full_gt_64x64", r.random((64, 64)).astype(np.float32), np.ones((64, 64), bool)))
+    g = np.zeros((80, 100), bool); g[37, 61] = True
+    cases.append(("single_px_80x100", smooth(80, 100), g))
+    thr = torch.linspace(0, 1 - 1e-10, 255).numpy()
+    p = thr[r.integers(0, 255, (120, 90))].astype(np.float32)
+    p[:5] = 0.0; p[-5:] = 1.0
+    cases.append(("on_thresholds_120x90", p, ell(120, 90, 60, 45, 40, 30)))
+    g = ell(256, 256, 120, 140, 70, 50) | ell(256, 256, 200, 60, 20, 30)
+    p = np.clip(g * 0.85 + 0.15 * smooth(256, 256) + 0.05 * r.standard_normal((256, 256)), 0, 1).astype(np.float32)
+    cases.append(("two_blobs_256", p, g))
+    g = np.zeros((33, 47), bool); g[5:20, 0] = True
+    cases.append(("left_column_33x47", smooth(33, 47), g))
+    p = np.zeros((40, 52), np.float32); p[10:30, 12:40] = 1.0
+    cases.append(("binary_pred_40x52", p, ell(40, 52, 20, 26, 11, 15)))
+    return [(n, p.astype(np.float32), g.astype(np.float64)) for n, p, g in cases]
+
+
+def gen_metrics():
+    """tests/golden/metrics.npz: the reference's EvaluationMetrics (metrics.py:213-424) on CPU
+    (device=None) for every metric_cases() pair, per-image values + the aggregate dict."""
+    from synth_sod.model_training.metrics import EvaluationMetrics
+    out = {}
+    names = []
+    full = EvaluationMetrics(device=None)
+    for name, p, g in metric_cases():
+        em = EvaluationMetrics(device=None)
+        em.step(torch.from_numpy(p.copy()), torch.from_numpy(g.copy()))
+        full.step(torch.from_numpy(p.copy()), torch.from_numpy(g.copy()))
+        sm = EvaluationMetrics(device=None, sm_only=True)
+        sm.step(torch.from_numpy(p.copy()), torch.from_numpy(g.copy()))
+        vals = [em.metrics["mae"][0], em.metrics["max_f"][0], em.metrics["avg_f"][0], em.metrics["s_score"][0],
+                float(np.mean(em.emeasure.metrics["changeable_ems"][0])), float(em.weighted_fmeasure.metrics["weighted_fms"][0])]
+        out[f"{name}/pred"] = p
+        out[f"{name}/gt"] = g
+        out[f"{name}/values"] = np.array(vals, np.float64)
+        out[f"{name}/sm_only"] = np.array([sm.metrics["s_score"][0]], np.float64)
+        names.append(name)
+    agg = full.compute_metrics()
+    out["aggregate_keys"] = np.array(list(agg.keys()))
+    out["aggregate"] = np.array([float(v) for v in agg.values()], np.float64)
+    out["names"] = np.array(names)
+    np.savez_compressed(HERE / "metrics.npz", **out)
+    for n in names:
+        print(n, out[f"{n}/values"])
+
+
 def main():
     _install_shims()
+    if "--metrics" in sys.argv:
+        gen_metrics()
+        return
     if "--dinol" in sys.argv:
         torch.set_num_threads(os.cpu_count())
         gen_dinol()

@@ -124,7 +124,7 @@ def test_postprocess_antialias_resize(hw):
     h, w = S - 2 * ph, S - 2 * pw
     tmp = torch.empty(3, h, W0, device="cuda")
     out = torch.empty(3, H0, W0, device="cuda")
-    lib()("s3od_sigmoid_unpad_resize", logits, S, S, ph, pw, h, w, H0, W0, tmp, out, stream())
+    lib()("s3od_sigmoid_unpad_resize", logits, 3, S, S, ph, pw, h, w, H0, W0, tmp, out, stream())
     m = torch.sigmoid(logits.cpu())[0]
     if ph > 0:
         m = m[:, ph:-ph, :]

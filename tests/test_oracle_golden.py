@@ -159,3 +159,50 @@ def test_dinol_train_step_single_mask_loss():
     assert "seg_head.classifier_head.4.weight" in nograd
     for n, v in zip(g["bn_names"], g["bn_values"]):
         assert rel(sd[n].numpy(), v) < 1e-4, n
+
+
+# ---------------------------------------------------------------- evaluation metrics (f4)
+METRIC_TOL = {"mae": 1e-12, "max_f": 1e-7, "avg_f": 5e-7, "s_score": 5e-7, "em": 1e-12, "wfm": 1e-12}
+
+
+def test_metrics_oracle_matches_reference_goldens():
+    """oracle/metrics_oracle.py vs the reference's EvaluationMetrics run on CPU (metrics.npz)."""
+    from oracle import metrics_oracle as M
+    d = np.load(GOLDEN / "metrics.npz")
+    per = []
+    for n in d["names"]:
+        r = M.step(d[f"{n}/pred"], d[f"{n}/gt"])
+        v = np.array([r[k] for k in M.KEYS])
+        g = d[f"{n}/values"]
+        per.append(v)
+        for i, k in enumerate(M.KEYS):
+            if np.isnan(g[i]):
+                assert np.isnan(v[i]), (n, k)
+            else:
+                assert abs(v[i] - g[i]) <= METRIC_TOL[k] * max(1.0, abs(g[i])), (n, k, v[i], g[i])
+        s = M.step(d[f"{n}/pred"], d[f"{n}/gt"], sm_only=True)["s_score"]
+        assert (np.isnan(s) and np.isnan(d[f"{n}/sm_only"][0])) or abs(s - d[f"{n}/sm_only"][0]) < 5e-7
+    agg = dict(zip(d["aggregate_keys"], d["aggregate"]))
+    per = np.array(per)
+    for i, k in enumerate(("MAE", "MaxF", "AvgF", "Sm", "Em", "wF")):
+        a, b = np.mean(per[:, i]), agg[k]
+        assert (np.isnan(a) and np.isnan(b)) or abs(a - b) < 1e-6, k
+
+
+def test_edt_restatement_matches_scipy_ties():
+    """The distance-transform algorithm the HIP kernel runs picks scipy's nearest foreground pixel,
+    ties included (so the weighted-F 'Et' gather is identical)."""
+    from scipy.ndimage import distance_transform_edt
+    from oracle.metrics_oracle import edt_nearest
+    r = np.random.default_rng(4)
+    for t in range(25):
+        H, W = r.integers(4, 26, 2)
+        fg = r.random((H, W)) < r.uniform(0.02, 0.35)
+        if t % 5 == 0:
+            yy, xx = np.mgrid[:H, :W]
+            fg = ((yy - H / 2) ** 2 / 9 + (xx - W / 3) ** 2 / 16) < 1
+        if not fg.any():
+            fg[H // 2, W // 2] = True
+        _, idx = distance_transform_edt(fg == 0, return_indices=True)
+        iy, ix = edt_nearest(fg)
+        assert (iy == idx[0]).all() and (ix == idx[1]).all()
