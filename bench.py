@@ -282,7 +282,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if use_dist:
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("nccl", device_id=dev, timeout=__import__("datetime").timedelta(seconds=int(os.environ.get("S3OD_RCCL_TIMEOUT_S", "1800"))))
 
     from s3od_amd.model import DPTSegmentation
     from s3od_amd.loss import LossModule, FOCAL_IOU

@@ -359,12 +359,12 @@ DEV f32x4 mma_f(float a, float b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16
 DEV float ldsf(const char* img, int row, int col) { return *(const float*)(img + Img<float>::at(row, col * 4)); }
 }  // namespace
 
-// dK, dV.  Workgroup = 4 waves x 32 keys of one (b,h); loop over 64-query tiles.
+// dK, dV.  Workgroup = 4 waves x 16*KS keys of one (b,h); loop over 64-query tiles.
 //   S  = Q K^T     (A = Q rows from LDS, B = K fragments in registers)   -> lane = key, regs = q
 //   dP = dO V^T    (A = dO rows from LDS, B = V fragments in registers)
 //   dV^T += dO^T P (A = dO^T via transposed LDS reads, B = P from the accumulators)
 //   dK^T += Q^T dS (A = Q^T via transposed LDS reads, B = dS from the accumulators)
-template <typename T>
+template <typename T, int KS>
 __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
                                                              const T* __restrict__ dO, const float* __restrict__ LSE,
                                                              const float* __restrict__ Dl, T* __restrict__ dK, T* __restrict__ dV,
@@ -381,13 +381,13 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const T* __restrict_
   const long ldo = (long)H * 64;
   const float* Lp = LSE + (long)bh * N;
   const float* Dp = Dl + (long)bh * N;
-  const int k0 = blockIdx.x * 128 + wave * 32;
+  const int k0 = blockIdx.x * (64 * KS) + wave * (16 * KS);
 
   constexpr int KK = F32 ? 16 : 2;
   typedef typename std::conditional<F32, float, bf16x8>::type frag;
-  frag kf[2][KK], vf[2][KK];
+  frag kf[KS][KK], vf[KS][KK];
 #pragma unroll
-  for (int ks = 0; ks < 2; ks++) {
+  for (int ks = 0; ks < KS; ks++) {
     int key = k0 + ks * 16 + li;
 #pragma unroll
     for (int kk = 0; kk < KK; kk++) {
@@ -401,11 +401,11 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const T* __restrict_
       }
     }
   }
-  f32x4 dk[4][2], dv[4][2];
+  f32x4 dk[4][KS], dv[4][KS];
 #pragma unroll
   for (int i = 0; i < 4; i++)
 #pragma unroll
-    for (int j = 0; j < 2; j++) { dk[i][j] = f32x4{0, 0, 0, 0}; dv[i][j] = f32x4{0, 0, 0, 0}; }
+    for (int j = 0; j < KS; j++) { dk[i][j] = f32x4{0, 0, 0, 0}; dv[i][j] = f32x4{0, 0, 0, 0}; }
 
   RowTile<T> tq, tdo;
   float lse_r = 0.f, dl_r = 0.f;
@@ -433,12 +433,12 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const T* __restrict_
     const float* dll = lsel + 64;
     // accumulators start at -LSE[q] / -delta[q] (q = qb*16 + 4g + i), so after the MFMAs
     // s = score - lse (log2 units) and dp = dO.v - delta
-    f32x4 s[4][2], dp[4][2];
+    f32x4 s[4][KS], dp[4][KS];
 #pragma unroll
     for (int qb = 0; qb < 4; qb++) {
       f32x4 nl = *(const f32x4*)(lsel + qb * 16 + 4 * g), nd = *(const f32x4*)(dll + qb * 16 + 4 * g);
 #pragma unroll
-      for (int ks = 0; ks < 2; ks++) { s[qb][ks] = nl; dp[qb][ks] = nd; }
+      for (int ks = 0; ks < KS; ks++) { s[qb][ks] = nl; dp[qb][ks] = nd; }
     }
 #pragma unroll
     for (int qb = 0; qb < 4; qb++) {
@@ -447,11 +447,11 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const T* __restrict_
         if constexpr (F32) {
           float a = ldsf(qs_, qb * 16 + li, kk * 4 + g), c = ldsf(dos, qb * 16 + li, kk * 4 + g);
 #pragma unroll
-          for (int ks = 0; ks < 2; ks++) { s[qb][ks] = mma_f(a, kf[ks][kk], s[qb][ks]); dp[qb][ks] = mma_f(c, vf[ks][kk], dp[qb][ks]); }
+          for (int ks = 0; ks < KS; ks++) { s[qb][ks] = mma_f(a, kf[ks][kk], s[qb][ks]); dp[qb][ks] = mma_f(c, vf[ks][kk], dp[qb][ks]); }
         } else {
           bf16x8 a = row_frag(qs_, qb * 16, kk, lane), c = row_frag(dos, qb * 16, kk, lane);
 #pragma unroll
-          for (int ks = 0; ks < 2; ks++) { s[qb][ks] = mma_bf(a, kf[ks][kk], s[qb][ks]); dp[qb][ks] = mma_bf(c, vf[ks][kk], dp[qb][ks]); }
+          for (int ks = 0; ks < KS; ks++) { s[qb][ks] = mma_bf(a, kf[ks][kk], s[qb][ks]); dp[qb][ks] = mma_bf(c, vf[ks][kk], dp[qb][ks]); }
         }
       }
     }
@@ -459,7 +459,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const T* __restrict_
 #pragma unroll
     for (int qb = 0; qb < 4; qb++)
 #pragma unroll
-      for (int ks = 0; ks < 2; ks++)
+      for (int ks = 0; ks < KS; ks++)
 #pragma unroll
         for (int i = 0; i < 4; i++) {
           float p = fexp2(s[qb][ks][i]);
@@ -477,20 +477,20 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const T* __restrict_
           for (int ds = 0; ds < 4; ds++) {
             float ao = ldsf(dos, qq, ds * 16 + li), aq = ldsf(qs_, qq, ds * 16 + li);
 #pragma unroll
-            for (int ks = 0; ks < 2; ks++) { dv[ds][ks] = mma_f(ao, s[qb][ks][i], dv[ds][ks]); dk[ds][ks] = mma_f(aq, dp[qb][ks][i], dk[ds][ks]); }
+            for (int ks = 0; ks < KS; ks++) { dv[ds][ks] = mma_f(ao, s[qb][ks][i], dv[ds][ks]); dk[ds][ks] = mma_f(aq, dp[qb][ks][i], dk[ds][ks]); }
           }
         }
     } else {
 #pragma unroll
       for (int qst = 0; qst < 2; qst++) {
-        bf16x8 pb[2], sb[2];
+        bf16x8 pb[KS], sb[KS];
 #pragma unroll
-        for (int ks = 0; ks < 2; ks++) { pb[ks] = pack8(s[2 * qst][ks], s[2 * qst + 1][ks]); sb[ks] = pack8(dp[2 * qst][ks], dp[2 * qst + 1][ks]); }
+        for (int ks = 0; ks < KS; ks++) { pb[ks] = pack8(s[2 * qst][ks], s[2 * qst + 1][ks]); sb[ks] = pack8(dp[2 * qst][ks], dp[2 * qst + 1][ks]); }
 #pragma unroll
         for (int ds = 0; ds < 4; ds++) {
           bf16x8 ao = tr_frag(dos, 32 * qst, ds * 16, lane), aq = tr_frag(qs_, 32 * qst, ds * 16, lane);
 #pragma unroll
-          for (int ks = 0; ks < 2; ks++) { dv[ds][ks] = mma_bf(ao, pb[ks], dv[ds][ks]); dk[ds][ks] = mma_bf(aq, sb[ks], dk[ds][ks]); }
+          for (int ks = 0; ks < KS; ks++) { dv[ds][ks] = mma_bf(ao, pb[ks], dv[ds][ks]); dk[ds][ks] = mma_bf(aq, sb[ks], dk[ds][ks]); }
         }
       }
     }
@@ -500,7 +500,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const T* __restrict_
   }
   // store: lane = key (li), rows d = ds*16 + 4g + i
 #pragma unroll
-  for (int ks = 0; ks < 2; ks++) {
+  for (int ks = 0; ks < KS; ks++) {
     int key = k0 + ks * 16 + li;
     if (key >= N) continue;
     T* dkr = dK + ((long)bh * N + key) * 64;
@@ -520,10 +520,10 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const T* __restrict_
   }
 }
 
-// dQ (w.r.t. the pre-scaled q).  Workgroup = 4 waves x 32 queries; loop over 64-key tiles.
+// dQ (w.r.t. the pre-scaled q).  Workgroup = 4 waves x 16*QS queries; loop over 64-key tiles.
 //   S^T = K Q^T, dP^T = V dO^T (B operands Q, dO in registers)  -> lane = q, regs = keys
 //   dQ^T += K^T dS^T            (A = K^T via transposed LDS reads, B = dS^T from accumulators)
-template <typename T>
+template <typename T, int QS>
 __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
                                                            const T* __restrict__ dO, const float* __restrict__ LSE,
                                                            const float* __restrict__ Dl, T* __restrict__ dQ, int N, int H) {
@@ -537,13 +537,13 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const T* __restrict__ 
   const T* Vp = V + (long)bh * N * 64;
   const T* dOp = dO + (long)b * N * (H * 64) + h * 64;
   const long ldo = (long)H * 64;
-  const int q0 = blockIdx.x * 128 + wave * 32;
+  const int q0 = blockIdx.x * (64 * QS) + wave * (16 * QS);
   constexpr int KK = F32 ? 16 : 2;
   typedef typename std::conditional<F32, float, bf16x8>::type frag;
-  frag qf[2][KK], of[2][KK];
-  float Lq[2], Dq[2];
+  frag qf[QS][KK], of[QS][KK];
+  float Lq[QS], Dq[QS];
 #pragma unroll
-  for (int qs = 0; qs < 2; qs++) {
+  for (int qs = 0; qs < QS; qs++) {
     int q = q0 + qs * 16 + li;
     Lq[qs] = q < N ? LSE[(long)bh * N + q] : INFINITY;
     Dq[qs] = q < N ? Dl[(long)bh * N + q] : 0.f;
@@ -559,12 +559,14 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const T* __restrict__ 
       }
     }
   }
-  f32x4 dq[4][2];
+  f32x4 dq[4][QS];
 #pragma unroll
-  for (int i = 0; i < 4; i++) { dq[i][0] = f32x4{0, 0, 0, 0}; dq[i][1] = f32x4{0, 0, 0, 0}; }
-  f32x4 nl[2], nd[2];   // C operands: -lse (log2 units), -delta of the lane's query column
+  for (int i = 0; i < 4; i++)
 #pragma unroll
-  for (int qs = 0; qs < 2; qs++) { nl[qs] = f32x4{-Lq[qs], -Lq[qs], -Lq[qs], -Lq[qs]}; nd[qs] = f32x4{-Dq[qs], -Dq[qs], -Dq[qs], -Dq[qs]}; }
+    for (int qs = 0; qs < QS; qs++) dq[i][qs] = f32x4{0, 0, 0, 0};
+  f32x4 nl[QS], nd[QS];   // C operands: -lse (log2 units), -delta of the lane's query column
+#pragma unroll
+  for (int qs = 0; qs < QS; qs++) { nl[qs] = f32x4{-Lq[qs], -Lq[qs], -Lq[qs], -Lq[qs]}; nd[qs] = f32x4{-Dq[qs], -Dq[qs], -Dq[qs], -Dq[qs]}; }
   RowTile<T> tk, tv;
   const int nkt = (N + 63) / 64;
   tk.load(Kp, 64, 0, N, tid); tv.load(Vp, 64, 0, N, tid);
@@ -576,20 +578,21 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const T* __restrict__ 
     if (more) { tk.load(Kp, 64, (kt + 1) * 64, N, tid); tv.load(Vp, 64, (kt + 1) * 64, N, tid); }
     const char* ks_ = smem + cur * 2 * I::BYTES;
     const char* vs_ = ks_ + I::BYTES;
-    f32x4 s[4][2], dp[4][2];
+    f32x4 s[4][QS], dp[4][QS];
 #pragma unroll
     for (int kb = 0; kb < 4; kb++) {
-      s[kb][0] = nl[0]; s[kb][1] = nl[1]; dp[kb][0] = nd[0]; dp[kb][1] = nd[1];
+#pragma unroll
+      for (int qs = 0; qs < QS; qs++) { s[kb][qs] = nl[qs]; dp[kb][qs] = nd[qs]; }
 #pragma unroll
       for (int kk = 0; kk < KK; kk++) {
         if constexpr (F32) {
           float a = ldsf(ks_, kb * 16 + li, kk * 4 + g), c = ldsf(vs_, kb * 16 + li, kk * 4 + g);
 #pragma unroll
-          for (int qs = 0; qs < 2; qs++) { s[kb][qs] = mma_f(a, qf[qs][kk], s[kb][qs]); dp[kb][qs] = mma_f(c, of[qs][kk], dp[kb][qs]); }
+          for (int qs = 0; qs < QS; qs++) { s[kb][qs] = mma_f(a, qf[qs][kk], s[kb][qs]); dp[kb][qs] = mma_f(c, of[qs][kk], dp[kb][qs]); }
         } else {
           bf16x8 a = row_frag(ks_, kb * 16, kk, lane), c = row_frag(vs_, kb * 16, kk, lane);
 #pragma unroll
-          for (int qs = 0; qs < 2; qs++) { s[kb][qs] = mma_bf(a, qf[qs][kk], s[kb][qs]); dp[kb][qs] = mma_bf(c, of[qs][kk], dp[kb][qs]); }
+          for (int qs = 0; qs < QS; qs++) { s[kb][qs] = mma_bf(a, qf[qs][kk], s[kb][qs]); dp[kb][qs] = mma_bf(c, of[qs][kk], dp[kb][qs]); }
         }
       }
     }
@@ -597,7 +600,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const T* __restrict__ 
 #pragma unroll
     for (int kb = 0; kb < 4; kb++)
 #pragma unroll
-      for (int qs = 0; qs < 2; qs++)
+      for (int qs = 0; qs < QS; qs++)
 #pragma unroll
         for (int i = 0; i < 4; i++) dp[kb][qs][i] *= fexp2(s[kb][qs][i]);
     if (kt * 64 + 64 > N) {   // last tile: zero dS of keys >= N (exp2(-lse) may overflow)
@@ -605,7 +608,10 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const T* __restrict__ 
       for (int kb = 0; kb < 4; kb++)
 #pragma unroll
         for (int i = 0; i < 4; i++)
-          if (kt * 64 + kb * 16 + 4 * g + i >= N) { dp[kb][0][i] = 0.f; dp[kb][1][i] = 0.f; }
+          if (kt * 64 + kb * 16 + 4 * g + i >= N) {
+#pragma unroll
+            for (int qs = 0; qs < QS; qs++) dp[kb][qs][i] = 0.f;
+          }
     }
     if constexpr (F32) {
 #pragma unroll
@@ -616,19 +622,21 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const T* __restrict__ 
 #pragma unroll
           for (int ds = 0; ds < 4; ds++) {
             float a = ldsf(ks_, key, ds * 16 + li);
-            dq[ds][0] = mma_f(a, dp[kb][0][i], dq[ds][0]);
-            dq[ds][1] = mma_f(a, dp[kb][1][i], dq[ds][1]);
+#pragma unroll
+            for (int qs = 0; qs < QS; qs++) dq[ds][qs] = mma_f(a, dp[kb][qs][i], dq[ds][qs]);
           }
         }
     } else {
 #pragma unroll
       for (int kst = 0; kst < 2; kst++) {
-        bf16x8 sb0 = pack8(dp[2 * kst][0], dp[2 * kst + 1][0]), sb1 = pack8(dp[2 * kst][1], dp[2 * kst + 1][1]);
+        bf16x8 sb[QS];
+#pragma unroll
+        for (int qs = 0; qs < QS; qs++) sb[qs] = pack8(dp[2 * kst][qs], dp[2 * kst + 1][qs]);
 #pragma unroll
         for (int ds = 0; ds < 4; ds++) {
           bf16x8 a = tr_frag(ks_, 32 * kst, ds * 16, lane);
-          dq[ds][0] = mma_bf(a, sb0, dq[ds][0]);
-          dq[ds][1] = mma_bf(a, sb1, dq[ds][1]);
+#pragma unroll
+          for (int qs = 0; qs < QS; qs++) dq[ds][qs] = mma_bf(a, sb[qs], dq[ds][qs]);
         }
       }
     }
@@ -637,7 +645,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const T* __restrict__ 
     cur ^= 1;
   }
 #pragma unroll
-  for (int qs = 0; qs < 2; qs++) {
+  for (int qs = 0; qs < QS; qs++) {
     int q = q0 + qs * 16 + li;
     if (q >= N) continue;
     T* r = dQ + ((long)bh * N + q) * 64;
@@ -667,13 +675,14 @@ int s3od_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* 
 int s3od_attn_bwd(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
                   float* delta, void* dq, void* dk, void* dv, int B, int H, int N, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  dim3 grid(cdiv(N, 128), B * H);
+  // 32 keys (dK/dV pass) / 32 queries (dQ pass) per wave: 64 per wave halves the LDS bytes per MFMA but
+  // needs > 256 registers -> one wave per SIMD: the whole backward measured 19 % (dK/dV) / 11 % (dQ) slower at N=4101
   DISPATCH_T(dtype, {
     hipLaunchKernelGGL(attn_delta_kernel<T>, dim3(cdiv((long)B * H * N * 8, 256)), dim3(256), 0, st, (const T*)o, (const T*)dout, delta, N, H, B * H);
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<T>, grid, dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse, delta,
-                       (T*)dk, (T*)dv, N, H);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<T>, grid, dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v, (const T*)dout, lse, delta,
-                       (T*)dq, N, H);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, 2>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v,
+                       (const T*)dout, lse, delta, (T*)dk, (T*)dv, N, H);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<T, 2>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v,
+                       (const T*)dout, lse, delta, (T*)dq, N, H);
   });
   return s3od_check_launch("attn_bwd");
 }

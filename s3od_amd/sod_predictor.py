@@ -105,7 +105,7 @@ class SODPredictor:
     @torch.no_grad()
     def predict(self, image: np.ndarray, threshold: float = 0.5) -> PredictionResult:
         from ._lib import lib, stream
-        image = np.ascontiguousarray(image, dtype=np.uint8)
+        image = np.require(image, np.uint8, ["C", "W"])
         pad_info = self.get_pad_info(image)
         S = self.image_size
         H0, W0 = image.shape[:2]

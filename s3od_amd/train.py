@@ -233,7 +233,10 @@ def fit(config, train_loader=None, val_loader=None, augment=None, val_augment=No
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if world > 1 and not dist.is_initialized():
-        dist.init_process_group("nccl", device_id=dev)
+        # a rank that stops answering (hung kernel, dead peer) fails the collective after this long
+        # instead of hanging the job: TORCH_NCCL_ASYNC_ERROR_HANDLING aborts the communicator
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        dist.init_process_group("nccl", device_id=dev, timeout=rccl_timeout())
     seed = int(be.get("seed", 42))
     seed_everything(seed)
     if train_loader is None:
@@ -268,6 +271,14 @@ def fit(config, train_loader=None, val_loader=None, augment=None, val_augment=No
     stopper = EarlyStop(**es_cfg) if es_cfg else None
     history = []
     epoch = start_epoch - 1
+    # non-finite loss guard: counted on device every micro-step, checked (one sync) every
+    # `nan_check_every` steps and at each epoch end -> FloatingPointError naming the step
+    nan_every = int(be.get("nan_check_every", 50))
+    bad = torch.zeros((), dtype=torch.int32, device=dev)
+
+    def check_finite(where):
+        if int(bad) > 0:
+            raise FloatingPointError(f"non-finite training loss ({int(bad)} micro-batches) before {where}")
     for epoch in range(start_epoch, max_epochs):
         module.current_epoch_ = epoch
         if hasattr(train_loader, "sampler") and hasattr(train_loader.sampler, "set_epoch"):
@@ -282,12 +293,16 @@ def fit(config, train_loader=None, val_loader=None, augment=None, val_augment=No
             with ctx:
                 loss = module.training_step(batch, i)
                 (loss / accum).backward()
+            bad += (~torch.isfinite(loss.detach())).to(torch.int32)
+            if nan_every > 0 and (i + 1) % nan_every == 0:
+                check_finite(f"epoch {epoch} batch {i}")
             logs = module.flush_logs()
             _accumulate(acc, logs, batch["images"].shape[0])
             if last_micro:
                 opt.step()
                 model.zero_grad(set_to_none=False)
                 global_step += 1
+        check_finite(f"the end of epoch {epoch}")
         metrics = _epoch_means(acc)
         if val_loader is not None:
             model.eval()
@@ -310,8 +325,32 @@ def fit(config, train_loader=None, val_loader=None, augment=None, val_augment=No
             break
     if world > 1:
         dist.barrier()
+    evaluation = None
+    ev = ts.get("evaluation") or {}
+    if rank == 0 and ev.get("enabled") and topk.best_model_path:
+        evaluation = evaluate(ev, topk.best_model_path, log)
     return {"epochs": epoch + 1 - start_epoch, "global_step": global_step, "best_model_path": topk.best_model_path,
-            "history": history, "module": module, "optimizer": opt, "scheduler": sched}
+            "history": history, "module": module, "optimizer": opt, "scheduler": sched, "evaluation": evaluation}
+
+
+def rccl_timeout():
+    """Collective timeout (S3OD_RCCL_TIMEOUT_S, default 30 min, as torch.distributed's default)."""
+    import datetime
+    return datetime.timedelta(seconds=int(os.environ.get("S3OD_RCCL_TIMEOUT_S", "1800")))
+
+
+def evaluate(ev, best_model_path, log=print):
+    """train.py:24-55 EvaluationCallback.on_fit_end: score the best checkpoint on every test dataset
+    with SODPredictor + the device metrics (compute_metrics.process_dataset)."""
+    from .metrics import process_dataset
+    from .sod_predictor import SODPredictor
+    predictor = SODPredictor(best_model_path, int(ev.get("image_size", 1024)), device="cuda")
+    out = {}
+    for name in ev.get("datasets") or []:
+        out[name] = process_dataset(os.path.join(str(ev["input_dir"]), name), predictor)
+        log(f"\n{name} metrics:")
+        log(out[name])
+    return out
 
 
 def main(argv=None):

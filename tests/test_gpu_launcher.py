@@ -23,7 +23,7 @@ def _dataset(root, n=3, S=96):
         Image.fromarray(m).save(root / "masks" / f"im{i}.png")
 
 
-def _config(tmp_path, data, max_epochs, ckpt=None):
+def _config(tmp_path, data, max_epochs, ckpt=None, evaluate=False):
     from s3od_amd.loss import FOCAL_IOU
     return {
         "backend": {"seed": 42, "devices": 1, "max_epochs": max_epochs, "accumulate_grad_batches": 2},
@@ -38,6 +38,8 @@ def _config(tmp_path, data, max_epochs, ckpt=None):
             {"_target_": "torch.optim.lr_scheduler.CosineAnnealingLR", "T_max": 4, "eta_min": 1e-6}], "milestones": [1]},
         "train_stage": {"save_dir": str(tmp_path / "ckpt"), "experiment_name": "t", "checkpoint_path": ckpt,
                         "weights_only": False,
+                        "evaluation": {"input_dir": str(data.parent), "enabled": evaluate, "image_size": 96,
+                                       "datasets": [data.name]},
                         "early_stopping": {"monitor": "val_iou_loss_full_epoch", "min_delta": 1e-4, "patience": 50,
                                            "mode": "min"}},
     }
@@ -47,7 +49,10 @@ def test_fit_two_epochs_accumulate_and_resume(tmp_path):
     from s3od_amd.train import fit
     data = tmp_path / "data"
     _dataset(data)
-    out = fit(_config(tmp_path, data, 2), log=lambda s: print(s))
+    out = fit(_config(tmp_path, data, 2, evaluate=True), log=lambda s: print(s))
+    # EvaluationCallback.on_fit_end (train.py:30-55): the best checkpoint scored with the device metrics
+    ev = out["evaluation"][data.name]
+    assert set(ev) == {"MAE", "MaxF", "AvgF", "Sm", "Em", "wF"} and all(np.isfinite(v) for v in ev.values())
     assert out["epochs"] == 2
     assert out["global_step"] == 2                       # 2 micro-batches / accumulate 2, per epoch
     h = out["history"]
@@ -67,3 +72,19 @@ def test_fit_two_epochs_accumulate_and_resume(tmp_path):
     assert out2["epochs"] == 1 and out2["history"][0]["epoch"] == 2
     assert out2["global_step"] == 3
     assert float(next(iter(out2["optimizer"].state_dict()["state"].values()))["step"]) == 3.0
+
+
+def test_fit_stops_on_non_finite_loss(tmp_path, monkeypatch):
+    """The launcher's loss guard: a NaN loss raises FloatingPointError at the next check."""
+    from s3od_amd.lightning_module import SegmentationLightningModule
+    from s3od_amd.train import fit
+    data = tmp_path / "data"
+    _dataset(data)
+    cfg = _config(tmp_path, data, 1)
+    cfg["backend"]["nan_check_every"] = 1
+
+    def nan_step(self, batch, i):
+        return next(self.model.parameters()).sum() * float("nan")
+    monkeypatch.setattr(SegmentationLightningModule, "training_step", nan_step)
+    with pytest.raises(FloatingPointError):
+        fit(cfg, log=lambda s: None)
