@@ -76,11 +76,25 @@ def conv(name, B, H, Cin, Cout, k=3, act=0):
     report(name, 2.0 * B * H * H * Cout * Cin * k * k, timeit(f))
 
 
+def dgrad_conv(name, B, H, Cin, Cout, k=3):
+    dy, w = r(B, H, H, Cout), r(Cout, k, k, Cin)
+    out = torch.empty(B, H, H, Cin, device="cuda", dtype=torch.bfloat16)
+    f = lambda: lib()("s3od_conv_dgrad", BF16, B, H, H, Cin, H, H, Cout, k, k, 1, k // 2, dy, w, None, None, None, 0, None,
+                      None, out, None, None, None, stream())
+    report(name, 2.0 * B * H * H * Cout * Cin * k * k, timeit(f))
+
+
 def report(name, fl, t):
     print(f"cfg {os.environ.get('S3OD_GEMM_CFG', 'def'):>3} {name:40s} {t * 1e6:8.1f} us {fl / t / 1e12:7.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
+    if os.environ.get("SWEEP") == "conv64":
+        conv("conv fwd 64->64 3x3 @1024^2 bs16 relu", 16, 1024, 64, 64, act=1)
+        conv("conv fwd 64->96 3x3 @1024^2 bs16 relu", 16, 1024, 64, 96, act=1)
+        dgrad_conv("conv dgrad 64<-64 3x3 @1024^2 bs16", 16, 1024, 64, 64)
+        dgrad_conv("conv dgrad 64<-96 3x3 @1024^2 bs16", 16, 1024, 64, 96)
+        sys.exit(0)
     qkv()
     fwd("o_proj fwd N768 K768 (res f32, out f32, pre)", D, D, res_f32=True, out_f32=True, pre=True, scale=True)
     fwd("up fwd N3072 K768 (GELU, pre)", F, D, act=ACT_GELU, pre=True)
