@@ -24,21 +24,32 @@ __global__ void repack_kernel(const float* __restrict__ src, T* __restrict__ dst
 }
 
 // Multi-tensor form: every packed weight of the model in ONE launch (the fp32 masters change after
-// each optimizer step, so the whole set is re-packed per step).  tab: device int64 [T][6] =
-// {src ptr, dst ptr, O, I, KH*KW, dst element offset}; chunk_t / chunk_o map blocks -> (tensor, start).
+// each optimizer step, so the whole set is re-packed per step).  tab: device int64 [T][RPK_FIELDS] =
+// {src ptr, dst ptr, O, I, KH*KW, dst element offset, mode, dst leading dim}; chunk_t / chunk_o map
+// blocks -> (tensor, start).  mode 0: dst [O][KHW][I] (the conv / linear kernel layout);
+// mode 1: dst [I][KHW][ld] with column o (+offset) and the taps reversed — the stride-1 conv's
+// data-gradient weight (dx = conv(dy, w^T flipped)), several tensors may interleave their columns.
+constexpr int RPK_FIELDS = 8;
 template <typename T>
 __global__ void __launch_bounds__(256) repack_multi_kernel(const long* __restrict__ tab, const int* __restrict__ chunk_t,
                                                            const long* __restrict__ chunk_o, int chunk) {
   const int t = chunk_t[blockIdx.x];
   const long o0 = chunk_o[blockIdx.x];
-  const float* src = (const float*)tab[6 * t + 0];
-  T* dst = (T*)tab[6 * t + 1] + tab[6 * t + 5];
-  const int O = (int)tab[6 * t + 2], I = (int)tab[6 * t + 3], KHW = (int)tab[6 * t + 4];
+  const long* e = tab + (long)RPK_FIELDS * t;
+  const float* src = (const float*)e[0];
+  T* dst = (T*)e[1] + e[5];
+  const int O = (int)e[2], I = (int)e[3], KHW = (int)e[4], mode = (int)e[6];
+  const long ld = e[7];
   const long total = (long)O * I * KHW;
   const long o1 = min(total, o0 + chunk);
   for (long idx = o0 + threadIdx.x; idx < o1; idx += blockDim.x) {
-    int i = idx % I; long r = idx / I; int tp = r % KHW; int o = r / KHW;
-    dst[idx] = from_f<T>(src[((long)o * I + i) * KHW + tp]);
+    if (mode == 0) {
+      int i = idx % I; long r = idx / I; int tp = r % KHW; int o = r / KHW;
+      dst[idx] = from_f<T>(src[((long)o * I + i) * KHW + tp]);
+    } else {
+      int o = idx % O; long r = idx / O; int tp = r % KHW; int i = r / KHW;
+      dst[((long)i * KHW + tp) * ld + o] = from_f<T>(src[((long)o * I + i) * KHW + (KHW - 1 - tp)]);
+    }
   }
 }
 
@@ -434,8 +445,9 @@ int s3od_repack_weight(int dtype, const float* src, void* dst, int O, int I, int
   return s3od_check_launch("repack_weight");
 }
 
-// tab: device int64 [ntensors][6] (src f32*, dst T* (or f32* for dtype F32 / fp32 biases), O, I, KH*KW,
-// dst element offset); chunk_t / chunk_o: device table of nchunks blocks (chunk elements each)
+// tab: device int64 [ntensors][8] (src f32*, dst T* (or f32* for dtype F32 / fp32 biases), O, I, KH*KW,
+// dst element offset, mode (0 kernel layout, 1 transposed + tap-reversed), dst leading dim (mode 1));
+// chunk_t / chunk_o: device table of nchunks blocks (chunk elements each)
 int s3od_repack_multi(int dtype, const long* tab, const int* chunk_t, const long* chunk_o, int nchunks, int chunk, void* stream) {
   S3OD_REQUIRE(nchunks >= 0 && chunk > 0, "repack_multi: bad chunk table");
   if (nchunks == 0) return 0;

@@ -58,12 +58,20 @@ static inline ConvGeo make_class(ConvGeo g, int OH, int OW, int py, int px) {
 
 // maps a GEMM row m to the linear output-pixel (row) index of the stored tensor
 struct RowMap {
-  int mode;          // 0 dense, 1 tokens (skip prefix), 2 parity class
+  int mode;          // 0 dense, 1 tokens (skip prefix), 2 parity class, 3 spatial tiles
   int P, prefix;     // tokens: m = b*P + p -> b*(P+prefix) + prefix + p
   int RH, RW, OH, OW, s, py, px;   // class: (b,y',x') -> (b, py+s*y', px+s*x') in OH x OW
+                                   // tiles: RH x RW tiles of TH x TW pixels (TH = s, TW = py) over OH x OW;
+                                   //   m = tile*TH*TW + ty*TW + tx -> pixel, or -1 outside the image
   DEV long map(int m) const {
     if (mode == 0) return m;
     if (mode == 1) { int b = m / P; return (long)b * (P + prefix) + prefix + (m - b * P); }
+    if (mode == 3) {
+      const int per = s * py, tile = m / per, r = m - tile * per;
+      const int txi = tile % RW, t2 = tile / RW, tyi = t2 % RH, b = t2 / RH;
+      const int y = tyi * s + r / py, x = txi * py + r % py;
+      return (y < OH && x < OW) ? ((long)b * OH + y) * OW + x : -1;
+    }
     int hw = RH * RW; int b = m / hw; int r = m - b * hw; int yy = r / RW; int xx = r - yy * RW;
     return ((long)b * OH + (py + s * yy)) * OW + (px + s * xx);
   }
@@ -837,7 +845,8 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
     const bool fixed_cols = NT % (BN / 8) == 0;
     for_segments(ct, LDT, BM, BN, m0, n0, M, N, tid, NT, [&](int m, int n, const float* a, int, int) {
       float pv[8], v[8], o[8];
-      long orow = rm.map(m);
+      const long orow = rm.map(m);
+      if (orow < 0) return;                 // spatial-tile row outside the image (RowMap mode 3)
       if (fixed_cols) {
 #pragma unroll
         for (int e = 0; e < 8; e++) { pv[e] = a[e] + b8[e]; v[e] = pv[e] * s8[e] + h8[e]; }

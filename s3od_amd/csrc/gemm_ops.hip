@@ -94,6 +94,7 @@ template <typename T> struct EpiQKV {
 template <typename T> struct EpiHeads {
   float* logits; T* hsave; const float* b1; const float* w2; const float* b2;
   int M, HW, NM;
+  RowMap rm;                                                  // staged row -> pixel (mode 0 dense, 3 tiles)
   DEV void prepare(int) {}
   DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN, int NT) const {
     const int C = 32 * NM, SPR = 4 * NM;                      // channels / 8-channel segments per row
@@ -103,12 +104,14 @@ template <typename T> struct EpiHeads {
       for (int s = tid; s < segs; s += NT) {
         int r = s / SPR, c = (s - r * SPR) * 8, m = m0 + r;
         if (m >= M) continue;
+        const long px = rm.map(m);
+        if (px < 0) continue;
         const float4* src = (const float4*)(ct + r * LDT + c);
         float4 x0 = src[0], x1 = src[1];
         float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
         for (int e = 0; e < 8; e++) v[e] = fmaxf(v[e] + b1[c + e], 0.f);
-        store8<T>(hsave + (long)m * C + c, v);
+        store8<T>(hsave + px * C + c, v);
       }
     }
     // logit_k = b2[k] + sum_j relu(acc[32k + j] + b1[32k + j]) * w2[32k + j]; k is wave-uniform
@@ -116,6 +119,8 @@ template <typename T> struct EpiHeads {
       int k = s / BM, r = s - k * BM;
       int m = m0 + r;
       if (m >= M) continue;
+      const long px = rm.map(m);
+      if (px < 0) continue;
       const float4* row = (const float4*)(ct + r * LDT + 32 * k);
       const float* bb = b1 + 32 * k;
       const float* ww = w2 + 32 * k;
@@ -128,11 +133,157 @@ template <typename T> struct EpiHeads {
         acc += fmaxf(x.z + bb[4 * q + 2], 0.f) * ww[4 * q + 2];
         acc += fmaxf(x.w + bb[4 * q + 3], 0.f) * ww[4 * q + 3];
       }
-      int b = m / HW, pix = m - b * HW;
-      logits[((long)b * NM + k) * HW + pix] = acc;
+      const long b = px / HW, pix = px - b * HW;
+      logits[(b * NM + k) * HW + pix] = acc;
     }
   }
 };
+
+// ---------------------------------------------------------------- halo-tile 3x3 convolution
+// 3x3 / stride 1 / pad 1 NHWC bf16 conv with Cin = 64 for the full-resolution decoder maps, where
+// the implicit GEMM streams the whole [Cout][9*Cin] weight block from L2 for every 256-pixel tile
+// (288 B of weights per output pixel at Cout = 64) and re-stages a 9x-gathered A.  Here:
+//   * persistent workgroups (one per CU) keep ALL nine taps' weights resident in LDS;
+//   * one tile = 8 x 32 output pixels; its (8+2) x (32+2) x 64 input halo is written to LDS once
+//     and the nine taps read their A fragments at shifted positions; the NEXT tile's halo is
+//     prefetched into registers while the current tile computes (no barrier inside the tap loop);
+//   * 16-B chunks XOR-swizzled by (pixel & 7) / (cout & 7): conflict-free ds_read_b128 fragment
+//     reads for every tap offset (checked exhaustively against the gfx950 lane groups);
+//   * wave w computes output row w (32 pixels) x all Cout; the fp32 C tile is staged through the
+//     (consumed) halo region in row chunks and handed to the GEMM engine's block epilogues, with
+//     RowMap mode 3 mapping the tile-major virtual rows to pixels (rows outside the image skipped).
+constexpr int HT_TH = 8, HT_TW = 32, HT_HR = HT_TH + 2, HT_HC = HT_TW + 2, HT_PX = HT_HR * HT_HC;
+template <int COUT> struct HaloShape {
+  static constexpr int CIN = 64, CPP = CIN / 8;           // 16-B chunks per pixel / weight row
+  static constexpr int WTS = 9 * COUT * 128;              // resident weights [tap][cout][64] bf16
+  static constexpr int HALO = HT_PX * 128;                // halo image [px][64] bf16
+  static constexpr int LDT = COUT + 4;
+  static constexpr int CR = (HALO / (LDT * 4)) >= 128 ? 128 : 64;   // C rows staged per chunk
+  static_assert(CR * LDT * 4 <= HALO, "C chunk must fit the halo region");
+  static constexpr int LDS = WTS + HALO;
+  static_assert(LDS <= 160 * 1024, "halo conv LDS budget");
+  static constexpr int HCH = HT_PX * CPP, HPT = (HCH + 511) / 512;
+};
+DEV int swz16(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+template <int COUT, class EPI>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2)))
+conv3x3_halo_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EPI epi, int H, int W, int tiles_x, int tiles_y,
+                    int ntiles) {
+  typedef HaloShape<COUT> S;
+  constexpr int CPP = S::CPP;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* wts = smem;
+  char* halo = smem + S::WTS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  // tiles of this workgroup: XCD x = blockIdx % 8 owns the contiguous tile range [x*n/8, (x+1)*n/8)
+  // (neighbouring tiles share halo rows in that XCD's L2); its workgroups stride through it
+  const int nwg = gridDim.x, xcd = blockIdx.x & 7, wpx = (nwg + 7 - xcd) >> 3, wi = blockIdx.x >> 3;
+  const int t_beg = (int)((long)ntiles * xcd / 8), t_end = (int)((long)ntiles * (xcd + 1) / 8);
+
+  // all nine taps' weights -> LDS, w: [COUT][9][64]
+  for (int c = tid; c < 9 * COUT * CPP; c += 512) {
+    const int ch = c % CPP, r = c / CPP, co = r % COUT, tap = r / COUT;
+    *(uint4*)(wts + swz16(tap * COUT + co, ch)) = *(const uint4*)(w + ((long)co * 9 + tap) * 64 + ch * 8);
+  }
+  uint4 hr[S::HPT];
+  auto prefetch = [&](int tile) {
+    const int txi = tile % tiles_x, t2 = tile / tiles_x, tyi = t2 % tiles_y, b = t2 / tiles_y;
+    const int ty0 = tyi * HT_TH - 1, tx0 = txi * HT_TW - 1;
+#pragma unroll
+    for (int i = 0; i < S::HPT; i++) {
+      const int c = tid + 512 * i;
+      hr[i] = make_uint4(0, 0, 0, 0);
+      if (c < S::HCH) {
+        const int px = c / CPP, ch = c - px * CPP, hy = px / HT_HC, hx = px - hy * HT_HC;
+        const int gy = ty0 + hy, gx = tx0 + hx;
+        if (gy >= 0 && gy < H && gx >= 0 && gx < W) hr[i] = *(const uint4*)(x + (((long)b * H + gy) * W + gx) * 64 + ch * 8);
+      }
+    }
+  };
+  int tile = t_beg + wi;
+  if (tile < t_end) prefetch(tile);
+  constexpr int NB = COUT / 16;
+  const int swb0 = (((0 + lg) ^ (lr & 7)) << 4), swb1 = (((4 + lg) ^ (lr & 7)) << 4);   // B chunk offsets (kk = 0, 1)
+  for (; tile < t_end; tile += wpx) {
+#pragma unroll
+    for (int i = 0; i < S::HPT; i++) {
+      const int c = tid + 512 * i;
+      if (c < S::HCH) { const int px = c / CPP, ch = c - px * CPP; *(uint4*)(halo + swz16(px, ch)) = hr[i]; }
+    }
+    __syncthreads();
+    if (tile + wpx < t_end) prefetch(tile + wpx);     // next tile's halo in flight during the MFMAs
+    f32x4 acc[2][NB];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int j = 0; j < NB; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 3
+    for (int tap = 0; tap < 9; tap++) {
+      const int dy = tap / 3, dx = tap - dy * 3;
+      const int p0 = (wave + dy) * HT_HC + dx + lr;   // this lane's halo pixel for pb = 0
+      const char* wt = wts + (tap * COUT + lr) * 128;
+#pragma unroll
+      for (int kk = 0; kk < 2; kk++) {
+        bf16x8 fa[2], fb[NB];
+#pragma unroll
+        for (int pb = 0; pb < 2; pb++) fa[pb] = *(const bf16x8*)(halo + swz16(p0 + pb * 16, kk * 4 + lg));
+#pragma unroll
+        for (int nb = 0; nb < NB; nb++) fb[nb] = *(const bf16x8*)(wt + nb * 16 * 128 + (kk ? swb1 : swb0));
+#pragma unroll
+        for (int pb = 0; pb < 2; pb++)
+#pragma unroll
+          for (int nb = 0; nb < NB; nb++) acc[pb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nb], fa[pb], acc[pb][nb], 0, 0, 0);
+      }
+    }
+    __syncthreads();                                  // halo consumed: its region now stages C
+    // lane owns C[px = pb*16 + lr][n = nb*16 + 4*lg .. +3] of output row `wave`
+    float* ct = (float*)halo;
+    const int vbase = tile * (HT_TH * HT_TW);
+    constexpr int WPC = S::CR / HT_TW;               // waves (output rows) per staged chunk
+#pragma unroll
+    for (int c0 = 0; c0 < HT_TH; c0 += WPC) {
+      if (wave >= c0 && wave < c0 + WPC) {
+        const int rr = (wave - c0) * HT_TW;
+#pragma unroll
+        for (int pb = 0; pb < 2; pb++)
+#pragma unroll
+          for (int nb = 0; nb < NB; nb++)
+            *(float4*)(ct + (rr + pb * 16 + lr) * S::LDT + nb * 16 + 4 * lg) =
+                make_float4(acc[pb][nb][0], acc[pb][nb][1], acc[pb][nb][2], acc[pb][nb][3]);
+      }
+      __syncthreads();
+      epi(ct, S::LDT, vbase + c0 * HT_TW, 0, tid, S::CR, COUT, 512);
+      __syncthreads();
+    }
+  }
+}
+
+static RowMap halo_rowmap(int H, int W) {
+  RowMap r{}; r.mode = 3; r.s = HT_TH; r.py = HT_TW; r.RH = cdiv(H, HT_TH); r.RW = cdiv(W, HT_TW); r.OH = H; r.OW = W;
+  return r;
+}
+// built: Cin 64 -> Cout 64 (conv fwd, stride-1 dgrad with the transposed weight) and 64 -> 96 (mask heads)
+static bool halo_ok(int dtype, int C_in, int C_out) {
+  static const int knob = dev_knob("S3OD_CONV_HALO", 1);
+  return knob && dtype == S3OD_BF16 && C_in == 64 && (C_out == 64 || C_out == 96);
+}
+template <int COUT, class EPI>
+static int launch_halo(const bf16* x, const bf16* w, EPI epi, int B, int H, int W, hipStream_t st) {
+  typedef HaloShape<COUT> S;
+  auto kfn = conv3x3_halo_kernel<COUT, EPI>;
+  static bool attr = false;
+  if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS); attr = true; }
+  const int tx = cdiv(W, HT_TW), ty = cdiv(H, HT_TH);
+  const long tiles = (long)B * tx * ty;
+  if (tiles * HT_TH * HT_TW >= (1L << 31)) { s3od_set_error("halo conv: too many pixels"); return 22; }
+  static int ncu = 0;
+  if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
+  const int nwg = (int)std::min<long>(tiles, (long)ncu);       // one persistent workgroup per CU
+  hipLaunchKernelGGL(kfn, dim3(nwg), dim3(512), S::LDS, st, x, w, epi, H, W, tx, ty, (int)tiles);
+  return s3od_check_launch("conv3x3_halo");
+}
 
 template <int BM, int BN> struct Tile {};
 
@@ -280,6 +431,13 @@ int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int C
   ConvGeo g{}; g.B = B; g.SH = H; g.SW = W; g.SC = Cin; g.RH = OH; g.RW = OW; g.KH = KH; g.KW = KW; g.s = stride; g.p = pad;
   const int M = B * OH * OW, N = Cout, K = KH * KW * Cin;
   hipStream_t st = (hipStream_t)stream;
+  if (KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && !relu_in && !stats && Cout == 64 && halo_ok(dtype, Cin, Cout)) {
+    RowMap rm = halo_rowmap(H, W);
+    const int Mv = B * rm.RH * rm.RW * HT_TH * HT_TW;
+    EpiStd<bf16, bf16> e{(bf16*)out, (long)Cout, 0, bias, scale, shift, (const bf16*)res1, (long)Cout, (const bf16*)res2, (long)Cout,
+                         (bf16*)pre, (long)Cout, nullptr, act, Mv, N, rm, colsum};
+    return launch_halo<64>((const bf16*)x, (const bf16*)wp, e, B, H, W, st);
+  }
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(K, KT<T>::BK);
     auto go = [&](auto bn, auto rl) -> int {
@@ -308,8 +466,18 @@ int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int C
 int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW,
                     int stride, int pad, const void* dy, const void* wp,
                     const float* bias, const float* scale, const float* shift, int act, const void* res1,
-                    const void* res2, void* dx, void* pre, double* stats, float* colsum, void* stream) {
+                    const void* res2, void* dx, void* pre, double* stats, float* colsum, const void* wT, void* stream) {
   S3OD_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "conv_dgrad: channels %% 8");
+  if (wT && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && !stats && Cin == 64 && Cout == 64 &&
+      halo_ok(dtype, Cout, Cin)) {
+    // stride-1 3x3 data gradient = forward conv of dy with the transposed, tap-reversed weight wT
+    // ([Cin][3][3][Cout], packed by s3od_repack_multi mode 1) on the halo-tile kernel
+    RowMap rm = halo_rowmap(H, W);
+    const int Mv = B * rm.RH * rm.RW * HT_TH * HT_TW;
+    EpiStd<bf16, bf16> e{(bf16*)dx, (long)Cin, 0, bias, scale, shift, (const bf16*)res1, (long)Cin, (const bf16*)res2, (long)Cin,
+                         (bf16*)pre, (long)Cin, nullptr, act, Mv, Cin, rm, colsum};
+    return launch_halo<64>((const bf16*)dy, (const bf16*)wT, e, B, H, W, (hipStream_t)stream);
+  }
   ConvGeo g0{}; g0.B = B; g0.SH = OH; g0.SW = OW; g0.SC = Cout; g0.KH = KH; g0.KW = KW; g0.s = stride; g0.p = pad;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
@@ -382,6 +550,11 @@ int s3od_mask_heads_fwd(int dtype, int B, int H, int W, int NM, const void* feat
   ConvGeo g{}; g.B = B; g.SH = H; g.SW = W; g.SC = 64; g.RH = H; g.RW = W; g.KH = 3; g.KW = 3; g.s = 1; g.p = 1;
   const int M = B * H * W, N = 32 * NM, K = 9 * 64;
   hipStream_t st = (hipStream_t)stream;
+  if (N == 96 && halo_ok(dtype, 64, N)) {
+    RowMap rm = halo_rowmap(H, W);
+    EpiHeads<bf16> e{logits, (bf16*)hsave, b1, w2, b2, B * rm.RH * rm.RW * HT_TH * HT_TW, H * W, NM, rm};
+    return launch_halo<96>((const bf16*)feat, (const bf16*)w1p, e, B, H, W, st);
+  }
   DISPATCH_T(dtype, {
     constexpr int BM = 128;
     ConvFwdA<T, BM> la{}; la.x = (const T*)feat; la.g = g; la.M = M; la.relu = 0;

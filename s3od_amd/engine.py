@@ -97,11 +97,16 @@ class DPTEngine:
         def pack(name, O, I, KH=1, KW=1, dst=None, off=0):
             if dst is None:
                 dst = torch.empty((O, KH, KW, I), dtype=T, device=dev)
-            ents[self.dt].append((P[name], dst, off, O, I, KH * KW))
+            ents[self.dt].append((P[name], dst, off, O, I, KH * KW, 0, 0))
             return dst
 
+        def pack_dgrad(name, O, I, dst, off, ld):
+            """[I][3][3][ld] transposed + tap-reversed copy (column off..off+O): the weight of the
+            stride-1 3x3 conv's data gradient run as a forward conv (s3od_conv_dgrad's wT)."""
+            ents[self.dt].append((P[name], dst, off, O, I, 9, 1, ld))
+
         def copy32(name, dst, off, n):
-            ents[F32].append((P[name], dst, off, n, 1, 1))
+            ents[F32].append((P[name], dst, off, n, 1, 1, 0, 0))
 
         e = "encoder.embeddings."
         w["pe"] = pack(e + "patch_embeddings.weight", D, 3 * 16 * 16)
@@ -140,6 +145,12 @@ class DPTEngine:
         for k in range(nm):
             pack(m + f"mask_heads.{k}.0.weight", 32, 64, 3, 3, dst=heads, off=k * 32 * 9 * 64)
         w["heads1"] = heads
+        if self.dt == BF16:       # data-gradient weights of the halo-tile conv path (bf16 only)
+            w["c64T"] = torch.empty((64, 3, 3, 64), dtype=T, device=dev)
+            pack_dgrad(m + "upsample_2x.2.weight", 64, 64, w["c64T"], 0, 64)
+            w["heads1T"] = torch.empty((64, 3, 3, 32 * nm), dtype=T, device=dev)
+            for k in range(nm):
+                pack_dgrad(m + f"mask_heads.{k}.0.weight", 32, 64, w["heads1T"], 32 * k, 32 * nm)
         for key, n, per in (("heads1_b", "0.bias", 32), ("heads2", "2.weight", 32), ("heads2_b", "2.bias", 1)):
             w[key] = torch.empty(per * nm, dtype=torch.float32, device=dev)
             for k in range(nm):
@@ -147,8 +158,8 @@ class DPTEngine:
         tabs = []
         for dt, lst in ents.items():
             rows, ct, co = [], [], []
-            for t, (src, dst, off, O, I, KHW) in enumerate(lst):
-                rows.append([src.data_ptr(), dst.data_ptr(), O, I, KHW, off])
+            for t, (src, dst, off, O, I, KHW, mode, ld) in enumerate(lst):
+                rows.append([src.data_ptr(), dst.data_ptr(), O, I, KHW, off, mode, ld])
                 for o in range(0, O * I * KHW, self._REPACK_CHUNK):
                     ct.append(t); co.append(o)
             tabs.append((dt, dict(tab=torch.tensor(rows, dtype=torch.int64, device=dev),
@@ -179,7 +190,7 @@ class DPTEngine:
         if out is None:
             out = torch.empty((B, OH, OW, Cout_T), dtype=self.tdt, device=x.device)
         lib()("s3od_conv_dgrad", self.dt, B, OH, OW, Cout_T, IH, IW, Cin_T, k, k, s, p, x, w,
-              bias, None, None, act, None, None, out, None, None, None, stream())
+              bias, None, None, act, None, None, out, None, None, None, None, stream())
         return out
 
     def _bilinear(self, x, B, IH, IW, OH, OW, C):
@@ -401,19 +412,21 @@ class DPTEngine:
         ws = torch.empty(Cout * k * k * Cin, dtype=torch.float32, device=dy.device) if k > 1 else None
         lib()("s3od_conv_wgrad", self.dt, B, H, W, Cin, OH, OW, Cout, k, k, s, p, dy, x, int(relu_x), dw, ws, 0, stream())
 
-    def _dgrad_conv(self, dy, w, B, H, W, Cin, OH, OW, Cout, k, s, p, act=ACT_NONE, res1=None, out=None, colsum=None):
-        """dx [B,H,W,Cin] of a conv whose output grid is OH x OW with Cout channels (colsum: += column sums of dx)."""
+    def _dgrad_conv(self, dy, w, B, H, W, Cin, OH, OW, Cout, k, s, p, act=ACT_NONE, res1=None, out=None, colsum=None,
+                    wT=None):
+        """dx [B,H,W,Cin] of a conv whose output grid is OH x OW with Cout channels (colsum: += column sums of dx;
+        wT: the transposed tap-reversed weight of a 3x3 s1 conv -> the halo-tile kernel)."""
         if out is None:
             out = torch.empty((B, H, W, Cin), dtype=self.tdt, device=dy.device)
         lib()("s3od_conv_dgrad", self.dt, B, H, W, Cin, OH, OW, Cout, k, k, s, p, dy, w, None, None, None, act, res1,
-              None, out, None, None, colsum, stream())
+              None, out, None, None, colsum, wT, stream())
         return out
 
     def _dgrad_conv_res(self, dy, w, B, H, W, C, act, res1, res2):
         """3x3 s1 dgrad with RELU_BWD mask (res1 = the un-ReLU'd input) plus a residual gradient res2."""
         out = torch.empty((B, H, W, C), dtype=self.tdt, device=dy.device)
         lib()("s3od_conv_dgrad", self.dt, B, H, W, C, H, W, C, 3, 3, 1, 1, dy, w, None, None, None, act, res1,
-              res2, out, None, None, None, stream())
+              res2, out, None, None, None, None, stream())
         return out
 
     def _rcu_bwd(self, d_out, r, u, B, ctx, G):
@@ -479,11 +492,11 @@ class DPTEngine:
         self._wgrad_conv(dh, c64, B, HH, WW, 64, HH, WW, 32 * nm, 3, 1, 1, G["heads1_w"])
         # (bias gradients are column sums fused into the epilogue that produces each gradient)
         d64 = self._dgrad_conv(dh, W8["heads1"], B, HH, WW, 64, HH, WW, 32 * nm, 3, 1, 1, act=ACT_RELU_BWD, res1=c64,
-                               colsum=G[m + "upsample_2x.2.bias"])
+                               colsum=G[m + "upsample_2x.2.bias"], wT=W8.get("heads1T"))
         # ---- upsample_2x.2 conv 64->64 + ReLU
         self._wgrad_conv(d64, up, B, HH, WW, 64, HH, WW, 64, 3, 1, 1, G[m + "upsample_2x.2.weight"])
         dup = self._dgrad_conv(d64, W8["c64"], B, HH, WW, 64, HH, WW, 64, 3, 1, 1, act=ACT_RELU_BWD, res1=up,
-                               colsum=G[m + "upsample_2x.0.bias"])
+                               colsum=G[m + "upsample_2x.0.bias"], wT=W8.get("c64T"))
         # ---- upsample_2x.0 ConvTranspose 128->64 k4 s2 p1 + ReLU (conv view: Y=oc1 grid, X=up grid)
         self._wgrad_conv(oc1, dup, B, HH, WW, 64, H1, W1, 128, 4, 2, 1, G[m + "upsample_2x.0.weight"])
         doc1 = self._conv(dup, W8["up2x"], B, HH, WW, 64, 128, 4, 2, 1, colsum=G[m + "output_conv1.bias"])

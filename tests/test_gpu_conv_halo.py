@@ -1,0 +1,81 @@
+"""GPU: the halo-tile 3x3 convolution (csrc/gemm_ops.hip conv3x3_halo_kernel) that serves the bf16
+full-resolution decoder convs — upsample_2x.2 (64->64 + ReLU), the mask heads (64->96, fused ReLU +
+1x1 + hsave) and the stride-1 data gradient 64<-64 with the ReLU' mask and the bias column sums
+(64<-96 stays on the implicit GEMM and is checked here too) — against fp32 PyTorch convolutions of the same bf16 operands (reference semantics:
+nn.Conv2d in src/s3od/model.py:437-467).  Ragged sizes exercise partial tiles at the right and
+bottom edges (RowMap mode 3 drops the rows outside the image).  Tolerance: bf16 output rounding
+(max-abs <= 2e-2 of the output scale)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+BF16 = 1
+ACT_RELU, ACT_RELU_BWD = 1, 4
+
+
+def _close(a, b, tol=2e-2):
+    a, b = a.float(), b.float()
+    scale = b.abs().max().clamp_min(1e-6)
+    assert float((a - b).abs().max() / scale) <= tol, float((a - b).abs().max() / scale)
+
+
+def _nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 37, 45), (1, 64, 96), (3, 16, 33)])
+def test_conv_fwd_64_relu(B, H, W):
+    from s3od_amd._lib import lib, stream
+    g = torch.Generator(device="cuda").manual_seed(H * W)
+    x = torch.randn(B, 64, H, W, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(64, 64, 3, 3, device="cuda", generator=g) * 0.06).bfloat16()
+    bias = torch.randn(64, device="cuda", generator=g) * 0.1
+    ref = F.relu(F.conv2d(x.float(), w.float(), bias, padding=1))
+    out = torch.empty(B, H, W, 64, device="cuda", dtype=torch.bfloat16)
+    wp = w.permute(0, 2, 3, 1).contiguous()                      # [Cout][3][3][Cin]
+    lib()("s3od_conv_fwd", BF16, B, H, W, 64, H, W, 64, 3, 3, 1, 1, _nhwc(x), 0, wp, bias, None, None, ACT_RELU,
+          None, None, out, None, None, None, stream())
+    _close(out, _nhwc(ref))
+
+
+@pytest.mark.parametrize("cout_fwd", [64, 96])
+def test_conv_dgrad_relu_mask_and_colsum(cout_fwd):
+    """dx = conv_transpose(dy, W) * (res1 > 0), colsum += sum over pixels of dx."""
+    from s3od_amd._lib import lib, stream
+    B, H, W = 2, 40, 70
+    g = torch.Generator(device="cuda").manual_seed(cout_fwd)
+    dy = torch.randn(B, cout_fwd, H, W, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(cout_fwd, 64, 3, 3, device="cuda", generator=g) * 0.06).bfloat16()   # conv [Cout][Cin][3][3]
+    res1 = torch.randn(B, 64, H, W, device="cuda", generator=g).bfloat16()
+    dx_ref = F.conv_transpose2d(dy.float(), w.float(), padding=1) * (res1.float() > 0)
+    wp = w.permute(0, 2, 3, 1).contiguous()                                            # [Cout][3][3][Cin]
+    wT = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()                                 # [Cin][3][3][Cout], taps reversed
+    dx = torch.empty(B, H, W, 64, device="cuda", dtype=torch.bfloat16)
+    cs = torch.zeros(64, device="cuda")
+    lib()("s3od_conv_dgrad", BF16, B, H, W, 64, H, W, cout_fwd, 3, 3, 1, 1, _nhwc(dy), wp, None, None, None, ACT_RELU_BWD,
+          _nhwc(res1), None, dx, None, None, cs, wT, stream())
+    _close(dx, _nhwc(dx_ref))
+    # column sums are taken in fp32 before the bf16 rounding of dx: compare with the fp32 reference
+    ref_cs = dx_ref.sum((0, 2, 3))
+    tol = 2e-3 * dx_ref.abs().sum((0, 2, 3)).max()
+    assert float((cs - ref_cs).abs().max()) <= float(tol), (float((cs - ref_cs).abs().max()), float(tol))
+
+
+def test_mask_heads_fwd_halo():
+    from s3od_amd._lib import lib, stream
+    B, H, W, NM = 2, 50, 41, 3
+    g = torch.Generator(device="cuda").manual_seed(7)
+    feat = torch.randn(B, 64, H, W, device="cuda", generator=g).bfloat16()
+    w1 = (torch.randn(32 * NM, 64, 3, 3, device="cuda", generator=g) * 0.06).bfloat16()
+    b1 = torch.randn(32 * NM, device="cuda", generator=g) * 0.1
+    w2 = torch.randn(NM, 32, device="cuda", generator=g) * 0.2
+    b2 = torch.randn(NM, device="cuda", generator=g) * 0.1
+    h = F.relu(F.conv2d(feat.float(), w1.float(), b1, padding=1))                     # [B, 96, H, W]
+    ref = torch.stack([(h[:, 32 * k:32 * k + 32] * w2[k].view(1, 32, 1, 1)).sum(1) + b2[k] for k in range(NM)], 1)
+    logits = torch.empty(B, NM, H, W, device="cuda")
+    hsave = torch.empty(B * H * W, 32 * NM, device="cuda", dtype=torch.bfloat16)
+    lib()("s3od_mask_heads_fwd", BF16, B, H, W, NM, _nhwc(feat), w1.permute(0, 2, 3, 1).contiguous(), b1, w2.contiguous(),
+          b2, logits, hsave, stream())
+    _close(logits, ref, 3e-2)
+    _close(hsave.view(B, H, W, 32 * NM), _nhwc(h))

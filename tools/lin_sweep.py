@@ -77,11 +77,20 @@ def conv(name, B, H, Cin, Cout, k=3, act=0):
 
 
 def dgrad_conv(name, B, H, Cin, Cout, k=3):
-    dy, w = r(B, H, H, Cout), r(Cout, k, k, Cin)
+    dy, w, wT = r(B, H, H, Cout), r(Cout, k, k, Cin), r(Cin, k, k, Cout)
     out = torch.empty(B, H, H, Cin, device="cuda", dtype=torch.bfloat16)
     f = lambda: lib()("s3od_conv_dgrad", BF16, B, H, H, Cin, H, H, Cout, k, k, 1, k // 2, dy, w, None, None, None, 0, None,
-                      None, out, None, None, None, stream())
+                      None, out, None, None, None, wT, stream())
     report(name, 2.0 * B * H * H * Cout * Cin * k * k, timeit(f))
+
+
+def heads(name, B, H):
+    feat, w1 = r(B, H, H, 64), r(96, 3, 3, 64)
+    b1, w2, b2 = r(96, dt=torch.float32), r(3, 32, dt=torch.float32), r(3, dt=torch.float32)
+    logits = torch.empty(B, 3, H, H, device="cuda")
+    hsave = torch.empty(B * H * H, 96, device="cuda", dtype=torch.bfloat16)
+    f = lambda: lib()("s3od_mask_heads_fwd", BF16, B, H, H, 3, feat, w1, b1, w2, b2, logits, hsave, stream())
+    report(name, 2.0 * B * H * H * 96 * 576, timeit(f))
 
 
 def report(name, fl, t):
@@ -91,7 +100,7 @@ def report(name, fl, t):
 if __name__ == "__main__":
     if os.environ.get("SWEEP") == "conv64":
         conv("conv fwd 64->64 3x3 @1024^2 bs16 relu", 16, 1024, 64, 64, act=1)
-        conv("conv fwd 64->96 3x3 @1024^2 bs16 relu", 16, 1024, 64, 96, act=1)
+        heads("mask heads fwd 64->96 (+relu+1x1) @1024^2 bs16", 16, 1024)
         dgrad_conv("conv dgrad 64<-64 3x3 @1024^2 bs16", 16, 1024, 64, 64)
         dgrad_conv("conv dgrad 64<-96 3x3 @1024^2 bs16", 16, 1024, 64, 96)
         sys.exit(0)
