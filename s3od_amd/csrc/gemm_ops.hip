@@ -264,10 +264,14 @@ static RowMap halo_rowmap(int H, int W) {
   RowMap r{}; r.mode = 3; r.s = HT_TH; r.py = HT_TW; r.RH = cdiv(H, HT_TH); r.RW = cdiv(W, HT_TW); r.OH = H; r.OW = W;
   return r;
 }
-// built: Cin 64 -> Cout 64 (conv fwd, stride-1 dgrad with the transposed weight) and 64 -> 96 (mask heads)
+// built: Cin 64 -> Cout 64 (conv fwd, stride-1 dgrad with the transposed weight) and 64 -> 96 (mask heads).
+// Default (S3OD_CONV_HALO=1): the mask heads only.  In the training step the 64 -> 64 fwd / dgrad ran
+// 2 % / 3 % SLOWER than the implicit GEMM (r02k): with the weights resident, one workgroup fills a CU,
+// so the epilogue's dependent global loads (ReLU' mask, residual) are not hidden behind another
+// workgroup's MFMAs.  S3OD_CONV_HALO=2 enables them too (dev), 0 disables the path.
 static bool halo_ok(int dtype, int C_in, int C_out) {
   static const int knob = dev_knob("S3OD_CONV_HALO", 1);
-  return knob && dtype == S3OD_BF16 && C_in == 64 && (C_out == 64 || C_out == 96);
+  return dtype == S3OD_BF16 && C_in == 64 && ((C_out == 96 && knob >= 1) || (C_out == 64 && knob >= 2));
 }
 template <int COUT, class EPI>
 static int launch_halo(const bf16* x, const bf16* w, EPI epi, int B, int H, int W, hipStream_t st) {

@@ -10,6 +10,9 @@ import torch
 import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
+# The 64 -> 64 fwd / dgrad halo paths are opt-in (S3OD_CONV_HALO=2, read once per process): under the
+# default these cases check the implicit-GEMM path against the same fp32 reference; run this file
+# alone with S3OD_CONV_HALO=2 to check the halo kernel on them (done when it was built: 6/6 passed).
 BF16 = 1
 ACT_RELU, ACT_RELU_BWD = 1, 4
 
