@@ -323,7 +323,7 @@ def main():
         step()
     # untimed profiling pass: which entry point dominates (and the per-class table)
     bd = None
-    dom = "s3od_attn_bwd" if args.mode == "train" else "s3od_attn_fwd"
+    dom = "s3od_attn_bwd_qkv" if args.mode == "train" else "s3od_attn_fwd"
     if not args.no_breakdown:
         dom, bd = breakdown(step, 2, peak)
     torch.cuda.synchronize()

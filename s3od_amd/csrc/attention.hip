@@ -359,6 +359,70 @@ DEV f32x4 mma_f(float a, float b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16
 DEV float ldsf(const char* img, int row, int col) { return *(const float*)(img + Img<float>::at(row, col * 4)); }
 }  // namespace
 
+// Fused backward epilogue (s3od_attn_bwd_qkv): instead of dQ / dK / dV in [B*H, N, 64], write the
+// gradient of the QKV projection's output directly: d_qkv [B*N][3*H*64] (q | k | v column blocks,
+// the layout s3od_qkv_rope_fwd reads), with the inverse RoPE applied to the patch tokens of q and k
+// (tf:modeling_dinov3_vit.py:238-268: y = x cos + R(x) sin -> dx = cos dy + R^T(sin dy)), the 1/8 of
+// the pre-scaled q, and the q / v bias gradients as replicated column sums (k_proj has no bias).
+// Lane layout of the accumulators: token = lane's row, d = ds*16 + 4g + i, so the RoPE partner
+// d +- 32 is ds ^ 2 in the same lane.
+struct QkvSink {
+  void* dqkv; const float* cs; const float* sn; float* ws; int P;
+};
+template <typename T>
+DEV void qkv_sink_row(const QkvSink& o, int which, int b, int h, int H, int tok, int N, int g, const f32x4 (&val)[4], float scale,
+                      f32x4 (&csum)[4]) {
+  float out[4][4];
+  const bool rope = which < 2 && tok >= N - o.P;
+  if (rope) {
+    const int tp = tok - (N - o.P);
+#pragma unroll
+    for (int ds = 0; ds < 4; ds++) {
+      const float4 c = *(const float4*)(o.cs + (long)tp * 64 + ds * 16 + 4 * g);
+      const float4 sn = *(const float4*)(o.sn + (long)tp * 64 + (ds ^ 2) * 16 + 4 * g);
+      const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const float rt = ss[i] * val[ds ^ 2][i];
+        out[ds][i] = (cc[i] * val[ds][i] + (ds < 2 ? rt : -rt)) * scale;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int ds = 0; ds < 4; ds++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) out[ds][i] = val[ds][i] * scale;
+  }
+  T* row = (T*)o.dqkv + ((long)b * N + tok) * (3L * H * 64) + (long)which * H * 64 + h * 64;
+#pragma unroll
+  for (int ds = 0; ds < 4; ds++) {
+    T* dst = row + ds * 16 + 4 * g;
+    if constexpr (std::is_same<T, float>::value) *(float4*)dst = make_float4(out[ds][0], out[ds][1], out[ds][2], out[ds][3]);
+    else *(bf16x4*)dst = bf16x4{(bf16)out[ds][0], (bf16)out[ds][1], (bf16)out[ds][2], (bf16)out[ds][3]};
+#pragma unroll
+    for (int i = 0; i < 4; i++) csum[ds][i] += out[ds][i];
+  }
+}
+// sum the 16 row-lanes of each column group and add into replica `rep` of ws [q D | v D]
+DEV void qkv_sink_colsum(const QkvSink& o, int which, int h, int H, int rep, int lane, f32x4 (&csum)[4]) {
+#pragma unroll
+  for (int ds = 0; ds < 4; ds++)
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      float v = csum[ds][i];
+      v += __shfl_xor(v, 1); v += __shfl_xor(v, 2); v += __shfl_xor(v, 4); v += __shfl_xor(v, 8);
+      csum[ds][i] = v;
+    }
+  if ((lane & 15) == 0) {
+    const int D = H * 64, g = lane >> 4;
+    float* dst = o.ws + (long)rep * 2 * D + (which == 0 ? 0 : D) + h * 64 + 4 * g;
+#pragma unroll
+    for (int ds = 0; ds < 4; ds++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) atomicAdd(dst + ds * 16 + i, csum[ds][i]);
+  }
+}
+
 // dK, dV.  Workgroup = 4 waves x 16*KS keys of one (b,h); loop over 64-query tiles.
 //   S  = Q K^T     (A = Q rows from LDS, B = K fragments in registers)   -> lane = key, regs = q
 //   dP = dO V^T    (A = dO rows from LDS, B = V fragments in registers)
@@ -368,7 +432,7 @@ template <typename T, int KS>
 __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
                                                              const T* __restrict__ dO, const float* __restrict__ LSE,
                                                              const float* __restrict__ Dl, T* __restrict__ dK, T* __restrict__ dV,
-                                                             int N, int H) {
+                                                             int N, int H, QkvSink sink) {
   constexpr bool F32 = std::is_same<T, float>::value;
   typedef Img<T> I;
   __shared__ __attribute__((aligned(16))) char smem[2 * (2 * I::BYTES + 512)];
@@ -498,6 +562,21 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const T* __restrict_
     __syncthreads();
     cur ^= 1;
   }
+  if (sink.dqkv) {   // fused: dK (inverse RoPE) and dV straight into d_qkv + the v-bias column sums
+    f32x4 csk[4] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
+    f32x4 csv[4] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
+#pragma unroll
+    for (int ks = 0; ks < KS; ks++) {
+      const int key = k0 + ks * 16 + li;
+      if (key >= N) continue;
+      const f32x4 kv[4] = {dk[0][ks], dk[1][ks], dk[2][ks], dk[3][ks]};
+      const f32x4 vv[4] = {dv[0][ks], dv[1][ks], dv[2][ks], dv[3][ks]};
+      qkv_sink_row<T>(sink, 1, b, h, H, key, N, g, kv, LN2, csk);
+      qkv_sink_row<T>(sink, 2, b, h, H, key, N, g, vv, 1.f, csv);
+    }
+    if (sink.ws) qkv_sink_colsum(sink, 2, h, H, (blockIdx.y * gridDim.x + blockIdx.x) % S3OD_NREP, lane, csv);
+    return;
+  }
   // store: lane = key (li), rows d = ds*16 + 4g + i
 #pragma unroll
   for (int ks = 0; ks < KS; ks++) {
@@ -526,7 +605,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dkdv_kernel(const T* __restrict_
 template <typename T, int QS>
 __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
                                                            const T* __restrict__ dO, const float* __restrict__ LSE,
-                                                           const float* __restrict__ Dl, T* __restrict__ dQ, int N, int H) {
+                                                           const float* __restrict__ Dl, T* __restrict__ dQ, int N, int H,
+                                                           QkvSink sink) {
   constexpr bool F32 = std::is_same<T, float>::value;
   typedef Img<T> I;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * I::BYTES];
@@ -644,6 +724,18 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const T* __restrict__ 
     __syncthreads();
     cur ^= 1;
   }
+  if (sink.dqkv) {   // fused: dQ (inverse RoPE, x 1/8 for the raw q) into d_qkv + the q-bias column sums
+    f32x4 csq[4] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
+#pragma unroll
+    for (int qs = 0; qs < QS; qs++) {
+      const int q = q0 + qs * 16 + li;
+      if (q >= N) continue;
+      const f32x4 qv[4] = {dq[0][qs], dq[1][qs], dq[2][qs], dq[3][qs]};
+      qkv_sink_row<T>(sink, 0, b, h, H, q, N, g, qv, 0.125f, csq);
+    }
+    if (sink.ws) qkv_sink_colsum(sink, 0, h, H, (blockIdx.y * gridDim.x + blockIdx.x) % S3OD_NREP, lane, csq);
+    return;
+  }
 #pragma unroll
   for (int qs = 0; qs < QS; qs++) {
     int q = q0 + qs * 16 + li;
@@ -668,22 +760,57 @@ int s3od_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* 
   });
   return s3od_check_launch("attn_fwd");
 }
+}  // extern "C"
 
+namespace {
+__global__ void qkv_fold_kernel(const float* __restrict__ ws, float* __restrict__ a, float* __restrict__ b, int D) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * D) return;
+  float s = 0.f;
+  for (int r = 0; r < S3OD_NREP; r++) s += ws[(long)r * 2 * D + i];
+  if (i < D) { if (a) a[i] += s; }
+  else if (b) b[i - D] += s;
+}
+
+template <typename T>
+void launch_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse, float* delta,
+                void* dq, void* dk, void* dv, QkvSink sink, int B, int H, int N, hipStream_t st) {
+  // 32 keys (dK/dV pass) / 32 queries (dQ pass) per wave: 64 per wave halves the LDS bytes per MFMA but
+  // needs > 256 registers -> one wave per SIMD: the whole backward measured 19 % (dK/dV) / 11 % (dQ) slower at N=4101
+  hipLaunchKernelGGL(attn_delta_kernel<T>, dim3(cdiv((long)B * H * N * 8, 256)), dim3(256), 0, st, (const T*)o, (const T*)dout, delta, N, H, B * H);
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, 2>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v,
+                     (const T*)dout, lse, delta, (T*)dk, (T*)dv, N, H, sink);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<T, 2>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v,
+                     (const T*)dout, lse, delta, (T*)dq, N, H, sink);
+}
+}  // namespace
+
+extern "C" {
 
 // backward: o, do: [B, N, H*64]; q,k,v: [B*H, N, 64]; lse, delta(workspace): [B*H, N] fp32
 // outputs dq = dS.K (dS in natural units; the caller scales by 1/8 for d(rope(q))), dk, dv: [B*H, N, 64]
 int s3od_attn_bwd(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
                   float* delta, void* dq, void* dk, void* dv, int B, int H, int N, void* stream) {
-  hipStream_t st = (hipStream_t)stream;
-  // 32 keys (dK/dV pass) / 32 queries (dQ pass) per wave: 64 per wave halves the LDS bytes per MFMA but
-  // needs > 256 registers -> one wave per SIMD: the whole backward measured 19 % (dK/dV) / 11 % (dQ) slower at N=4101
-  DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(attn_delta_kernel<T>, dim3(cdiv((long)B * H * N * 8, 256)), dim3(256), 0, st, (const T*)o, (const T*)dout, delta, N, H, B * H);
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, 2>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v,
-                       (const T*)dout, lse, delta, (T*)dk, (T*)dv, N, H);
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<T, 2>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v,
-                       (const T*)dout, lse, delta, (T*)dq, N, H);
-  });
+  QkvSink none{};
+  DISPATCH_T(dtype, { launch_bwd<T>(q, k, v, o, dout, lse, delta, dq, dk, dv, none, B, H, N, (hipStream_t)stream); });
   return s3od_check_launch("attn_bwd");
+}
+
+// backward fused with the QKV+RoPE projection's output gradient: d_qkv [B*N][3*H*64] (T) with the
+// inverse RoPE on the last P tokens (cos_t / sin_t: [P][64] fp32, the forward's tables), q x 1/8,
+// and dbq / dbv (fp32 [H*64], nullable) += column sums; ws: S3OD_NREP * 2 * H*64 floats (nullable
+// when both bias gradients are null).  Replaces s3od_attn_bwd + s3od_qkv_unrope.
+int s3od_attn_bwd_qkv(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
+                      float* delta, const float* cos_t, const float* sin_t, int P, void* dqkv, float* dbq, float* dbv,
+                      float* ws, int B, int H, int N, void* stream) {
+  S3OD_REQUIRE(dqkv && cos_t && sin_t && P >= 0 && P <= N, "attn_bwd_qkv: bad arguments");
+  S3OD_REQUIRE(ws || (!dbq && !dbv), "attn_bwd_qkv: bias gradients need the workspace");
+  hipStream_t st = (hipStream_t)stream;
+  const int D = 64 * H;
+  if (ws) (void)hipMemsetAsync(ws, 0, sizeof(float) * S3OD_NREP * 2 * D, st);
+  QkvSink sink{dqkv, cos_t, sin_t, ws, P};
+  DISPATCH_T(dtype, { launch_bwd<T>(q, k, v, o, dout, lse, delta, nullptr, nullptr, nullptr, sink, B, H, N, st); });
+  if (ws) hipLaunchKernelGGL(qkv_fold_kernel, dim3(cdiv(2 * D, 256)), dim3(256), 0, st, ws, dbq, dbv, D);
+  return s3od_check_launch("attn_bwd_qkv");
 }
 }  // extern "C"

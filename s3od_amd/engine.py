@@ -562,9 +562,6 @@ class DPTEngine:
         dxm = _E(None, (B, Nt, D), torch.float32, dev)
         dxi = _E(None, (B, Nt, D), torch.float32, dev)
         dqkv = _E(None, (M, 3 * D), T, dev)
-        dq = _E(None, (B * H, Nt, 64), T, dev)
-        dk = torch.empty_like(dq)
-        dv = torch.empty_like(dq)
         delta = _E(None, (B * H, Nt), torch.float32, dev)
         qv_ws = _E(None, (32 * 2 * D,), torch.float32, dev)     # S3OD_NREP replicas of the q/v bias partials
         red_ws = _E(None, (32 * 2 * D,), torch.float32, dev)    # same, for LayerNorm / LayerScale parameter grads
@@ -592,9 +589,9 @@ class DPTEngine:
             self._wgrad_lin(du, s["o"], D, D, M, G[p + "attention.o_proj.weight"])
             do = dh
             self._dgrad_lin(du, W8[f"o{i}"], M, D, D, do)
-            L("s3od_attn_bwd", dt, s["q"], s["k"], s["v"], s["o"], do, s["lse"], delta, dq, dk, dv, B, H, Nt, st)
-            L("s3od_qkv_unrope", dt, dq, dk, dv, ctx.t["cos"], ctx.t["sin"], dqkv, G[p + "attention.q_proj.bias"],
-              G[p + "attention.v_proj.bias"], qv_ws, B, Nt, NP, H, st)
+            # attention backward with the inverse RoPE / q scale / q,v bias sums fused into its stores
+            L("s3od_attn_bwd_qkv", dt, s["q"], s["k"], s["v"], s["o"], do, s["lse"], delta, ctx.t["cos"], ctx.t["sin"], NP,
+              dqkv, G[p + "attention.q_proj.bias"], G[p + "attention.v_proj.bias"], qv_ws, B, H, Nt, st)
             self._wgrad_lin(dqkv, s["h1"], 3 * D, D, M, G[f"qkv_w{i}"])
             dh1 = dh
             self._dgrad_lin(dqkv, W8[f"qkv{i}"], M, D, 3 * D, dh1)

@@ -99,3 +99,39 @@ def test_attention_bf16_c3_shape():
 
 def test_attention_bf16_c5_shape():
     _run(4, 12, 16389, seed=12)
+
+
+def test_attn_bwd_qkv_fused_equals_separate_path():
+    """s3od_attn_bwd_qkv (the engine's path) == s3od_attn_bwd + s3od_qkv_unrope on the same inputs:
+    d_qkv within bf16 rounding (the fused path skips the intermediate bf16 dq/dk/dv), bias sums
+    within fp32 summation order."""
+    from s3od_amd._lib import lib, stream
+    B, H, N, P = 2, 12, 1029, 1024
+    D = 64 * H
+    g = torch.Generator(device="cuda").manual_seed(3)
+    r = lambda *s: (torch.randn(*s, device="cuda", generator=g) * 0.5).to(torch.bfloat16)
+    q, k, v = r(B * H, N, 64), r(B * H, N, 64), r(B * H, N, 64)
+    q = (q.float() * 0.18).to(torch.bfloat16)
+    o = torch.empty(B, N, D, device="cuda", dtype=torch.bfloat16)
+    lse = torch.empty(B * H, N, device="cuda")
+    lib()("s3od_attn_fwd", 1, q, k, v, o, lse, B, H, N, stream())
+    do = r(B, N, D)
+    th = torch.rand(P, 32, device="cuda", generator=g) * 6.28
+    cs = torch.cat([th.cos(), th.cos()], 1).contiguous()
+    sn = torch.cat([th.sin(), th.sin()], 1).contiguous()
+    delta = torch.empty(B * H, N, device="cuda")
+    dq, dk, dv = (torch.empty(B * H, N, 64, device="cuda", dtype=torch.bfloat16) for _ in range(3))
+    ws = torch.empty(32 * 2 * D, device="cuda")
+    a = torch.empty(B * N, 3 * D, device="cuda", dtype=torch.bfloat16)
+    bq_a, bv_a = torch.zeros(D, device="cuda"), torch.zeros(D, device="cuda")
+    lib()("s3od_attn_bwd", 1, q, k, v, o, do, lse, delta, dq, dk, dv, B, H, N, stream())
+    lib()("s3od_qkv_unrope", 1, dq, dk, dv, cs, sn, a, bq_a, bv_a, ws, B, N, P, H, stream())
+    f = torch.empty_like(a)
+    bq_f, bv_f = torch.zeros(D, device="cuda"), torch.zeros(D, device="cuda")
+    lib()("s3od_attn_bwd_qkv", 1, q, k, v, o, do, lse, delta, cs, sn, P, f, bq_f, bv_f, ws, B, H, N, stream())
+    torch.cuda.synchronize()
+    af, ff = a.float(), f.float()
+    assert float((af - ff).abs().max() / af.abs().max()) < 1e-2
+    assert float((af - ff).norm() / af.norm()) < 4e-3
+    for x, y in ((bq_a, bq_f), (bv_a, bv_f)):
+        assert float((x - y).abs().max() / x.abs().max()) < 1e-2

@@ -26,7 +26,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 tag = sys.argv[1]
 kre = re.compile(sys.argv[2] if len(sys.argv) > 2 else r"attn_(bwd|delta)")
-entry = sys.argv[3] if len(sys.argv) > 3 else "s3od_attn_bwd"
+entry = sys.argv[3] if len(sys.argv) > 3 else "s3od_attn_bwd_qkv"
 steps = int(sys.argv[4]) if len(sys.argv) > 4 else 4       # 1 warm-up + 3 timed steps traced
 src = ROOT / "gpurun_out" / f"prof_{tag}"
 dst = ROOT / "profiles"

@@ -45,6 +45,9 @@ def cost(name, a):
     if n == "attn_bwd":
         B, H, N = a[11:14]
         return "mfma", 10.0 * B * H * N * N * 64
+    if n == "attn_bwd_qkv":
+        B, H, N = a[15:18]
+        return "mfma", 10.0 * B * H * N * N * 64
     # ---- memory-bound
     if n == "layernorm_fwd":
         dt, M = a[0], a[7]
@@ -103,6 +106,7 @@ CLASS = {
     "linear_fwd": "ViT/1x1 linear fwd", "qkv_rope_fwd": "ViT/1x1 linear fwd", "linear_dgrad": "linear dgrad",
     "linear_wgrad": "linear wgrad", "conv_fwd": "conv fwd", "conv_dgrad": "conv dgrad + ConvT fwd",
     "conv_wgrad": "conv wgrad", "mask_heads_fwd": "conv fwd", "attn_fwd": "attention fwd", "attn_bwd": "attention bwd",
+    "attn_bwd_qkv": "attention bwd",
 }
 
 

@@ -44,6 +44,7 @@ REF = {
     "s3od_mask_loss_fwd": "MaskLossHandler.compute_multi_mask_losses + aux MSE: synth_sod/.../model_training/loss.py:155-275",
     "s3od_mask_loss_bwd": "gradient of the multi-mask loss w.r.t. pred_masks / pred_iou logits: loss.py:190-275",
     "s3od_attn_bwd": "SDPA backward (reference: implicit torch autograd)",
+    "s3od_attn_bwd_qkv": "SDPA backward + apply_rotary_pos_emb backward + q/k/v_proj output gradient in one pass (reference: implicit torch autograd of tf:modeling_dinov3_vit.py:238-268, 294-329)",
     "s3od_adamw_step": "torch.optim.AdamW(wd=0.05, betas=(0.9,0.999), eps=1e-8), 2 param groups: lightning_module.py:183-193",
     "s3od_sigmoid_unpad_resize": "remove_background post-processing: src/s3od/predictor.py:113-132, src/s3od/utils.py:32-37",
     "s3od_augment_sample": "get_transforms geometry (LongestMaxSize + PadIfNeeded + flip/affine/perspective/optical distortion) + Normalize, one launch per sample: synth_sod/src/synth_sod/model_training/transforms.py:12-64, 205-222",

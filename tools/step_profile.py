@@ -44,6 +44,9 @@ def flops(name, a):
     if name == "s3od_attn_bwd":
         B, H, N = a[11:14]
         return 10.0 * B * H * N * N * 64, f"B{B} H{H} N{N}"
+    if name == "s3od_attn_bwd_qkv":
+        B, H, N = a[15:18]
+        return 10.0 * B * H * N * N * 64, f"B{B} H{H} N{N}"
     return 0.0, ""
 
 
