@@ -289,6 +289,134 @@ static int launch_halo(const bf16* x, const bf16* w, EPI epi, int B, int H, int 
   return s3od_check_launch("conv3x3_halo");
 }
 
+// ---------------------------------------------------------------- halo-tile 3x3 weight gradient
+// dW[co][tap][ci] = sum_px dy[px][co] * x[px + tap][ci] for a 3x3 / stride 1 / pad 1 conv with Cin = 64
+// and Cout = 64 / 96 (the full-resolution decoder convs).  The implicit-GEMM wgrad tiles N = 9*64 into
+// 128-column blocks, so every 64-pixel K tile is fetched once per N block: ~7x the unique bytes go
+// through L2 (measured: 57 % of wave time parked on vmcnt).  Here a persistent workgroup owns ALL
+// 9 x 64 x Cout outputs in registers and sweeps 8 x 32-pixel tiles: dy (256 px x Cout) and the x halo
+// (10 x 34 px x 64) are staged once per tile (register-prefetched one tile ahead) and every MFMA
+// operand is read with ds_read_b64_tr_b16 (K = pixels, permuted identically on both operands).
+// Waves: 4 (one per SIMD, up to 512 registers: the whole 9 x 64 x Cout fp32 block lives in registers),
+// 9 of the 36 (tap, ci-block) pairs each, all co blocks per wave so each B fragment feeds NCO MFMAs.  The partial sums are flushed once per
+// workgroup with fp32 atomics into the [co][tap][ci] workspace (wgrad_permute_add_kernel follows).
+template <int CO> struct WgShape {
+  static constexpr int DYB = 256 * CO * 2;                 // dy tile image [px][CO]
+  static constexpr int HXB = HT_PX * 128;                  // x halo image [px][64]
+  static constexpr int LDS = DYB + HXB;
+  static constexpr int DCH = 256 * CO / 8, HCH = HT_PX * 8;           // 16-B chunks to stage
+  static constexpr int NT = 256;                                       // 4 waves, one per SIMD
+  static constexpr int PT = (DCH + HCH + NT - 1) / NT;                 // 16-B chunks per thread
+  static_assert(LDS <= 160 * 1024, "halo wgrad LDS budget");
+};
+template <int CO> DEV int dy_at(int row, int byte) {       // conflict-free for the transposed reads
+  if constexpr (CO == 64) return row * 128 + ((((byte >> 4) ^ (row & 7)) << 4) | (byte & 15));
+  else return row * 192 + ((((byte >> 4) ^ ((row >> 1) & 3)) << 4) | (byte & 15));
+}
+DEV int hx_at(int row, int byte) { return row * 128 + ((((byte >> 4) ^ (row & 7)) << 4) | (byte & 15)); }
+// 16 columns x 32 rows fragment, transposed (rows = K, permuted: 4g + q and 16 + 4g + q)
+template <class AT> DEV bf16x8 trf(const char* img, int r0, int col0, int lane, AT at) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int byte = (col0 + 4 * p) * 2;
+  typedef __attribute__((address_space(3))) s16x4 lds4;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(img + at(r0 + 4 * g + q, byte)));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(img + at(r0 + 16 + 4 * g + q, byte)));
+  bf16x4 a = __builtin_bit_cast(bf16x4, lo), b = __builtin_bit_cast(bf16x4, hi);
+  return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+template <int CO, bool RELU>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+conv3x3_wgrad_halo_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, float* __restrict__ ws, int H, int W,
+                          int tiles_x, int tiles_y, int ntiles) {
+  typedef WgShape<CO> S;
+  constexpr int NCO = CO / 16, CPD = CO / 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* dyi = smem;
+  char* hxi = smem + S::DYB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nwg = gridDim.x, xcd = blockIdx.x & 7, wpx = (nwg + 7 - xcd) >> 3, wi = blockIdx.x >> 3;
+  const int t_beg = (int)((long)ntiles * xcd / 8), t_end = (int)((long)ntiles * (xcd + 1) / 8);
+  constexpr int NP = 9;                                  // (tap, ci-block) pairs of this wave: 9*wave ..
+  const int pair0 = NP * wave;
+  f32x4 acc[NP][NCO];
+#pragma unroll
+  for (int i = 0; i < NP; i++)
+#pragma unroll
+    for (int j = 0; j < NCO; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint4 pf[S::PT];
+  auto prefetch = [&](int tile) {
+    const int txi = tile % tiles_x, t2 = tile / tiles_x, tyi = t2 % tiles_y, b = t2 / tiles_y;
+    const int ty0 = tyi * HT_TH, tx0 = txi * HT_TW;
+#pragma unroll
+    for (int i = 0; i < S::PT; i++) {
+      const int c = tid + S::NT * i;
+      pf[i] = make_uint4(0, 0, 0, 0);
+      if (c < S::DCH) {                                   // dy tile: px = ty*32 + tx
+        const int px = c / CPD, ch = c - px * CPD, gy = ty0 + px / HT_TW, gx = tx0 + px % HT_TW;
+        if (gy < H && gx < W) pf[i] = *(const uint4*)(dy + (((long)b * H + gy) * W + gx) * CO + ch * 8);
+      } else if (c < S::DCH + S::HCH) {                   // x halo
+        const int c2 = c - S::DCH, px = c2 >> 3, ch = c2 & 7, hy = px / HT_HC, hx = px - hy * HT_HC;
+        const int gy = ty0 - 1 + hy, gx = tx0 - 1 + hx;
+        if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+          pf[i] = *(const uint4*)(x + (((long)b * H + gy) * W + gx) * 64 + ch * 8);
+          if (RELU) pf[i] = relu16<bf16>(pf[i]);
+        }
+      }
+    }
+  };
+  int tile = t_beg + wi;
+  if (tile < t_end) prefetch(tile);
+  for (; tile < t_end; tile += wpx) {
+#pragma unroll
+    for (int i = 0; i < S::PT; i++) {
+      const int c = tid + S::NT * i;
+      if (c < S::DCH) { const int px = c / CPD, ch = c - px * CPD; *(uint4*)(dyi + dy_at<CO>(px, ch * 16)) = pf[i]; }
+      else if (c < S::DCH + S::HCH) { const int c2 = c - S::DCH; *(uint4*)(hxi + hx_at(c2 >> 3, (c2 & 7) * 16)) = pf[i]; }
+    }
+    __syncthreads();
+    if (tile + wpx < t_end) prefetch(tile + wpx);
+    for (int ty = 0; ty < HT_TH; ty++) {                  // K step = one output row of 32 pixels
+      bf16x8 fa[NCO];
+#pragma unroll
+      for (int cb = 0; cb < NCO; cb++) fa[cb] = trf(dyi, ty * HT_TW, cb * 16, lane, dy_at<CO>);
+#pragma unroll
+      for (int j = 0; j < NP; j++) {
+        const int pr = pair0 + j, tap = pr >> 2, cib = pr & 3, tdy = tap / 3, tdx = tap - tdy * 3;
+        const bf16x8 fb = trf(hxi, (ty + tdy) * HT_HC + tdx, cib * 16, lane, hx_at);
+#pragma unroll
+        for (int cb = 0; cb < NCO; cb++) acc[j][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[cb], fb, acc[j][cb], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // flush: lane holds D[co = cb*16 + 4g + r][ci = cib*16 + li] of pair j -> ws[co][tap*64 + ci]
+  const int g = lane >> 4, li = lane & 15;
+#pragma unroll
+  for (int j = 0; j < NP; j++) {
+    const int pr = pair0 + j, tap = pr >> 2, cib = pr & 3;
+#pragma unroll
+    for (int cb = 0; cb < NCO; cb++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) atomicAdd(ws + (long)(cb * 16 + 4 * g + r) * 576 + tap * 64 + cib * 16 + li, acc[j][cb][r]);
+  }
+}
+
+template <int CO, bool RELU>
+static int launch_wgrad_halo(const bf16* dy, const bf16* x, float* ws, int B, int H, int W, hipStream_t st) {
+  typedef WgShape<CO> S;
+  auto kfn = conv3x3_wgrad_halo_kernel<CO, RELU>;
+  static bool attr = false;
+  if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS); attr = true; }
+  const int tx = cdiv(W, HT_TW), ty = cdiv(H, HT_TH);
+  const long tiles = (long)B * tx * ty;
+  static int ncu = 0;
+  if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
+  const int nwg = (int)std::min<long>(tiles, (long)ncu);    // one persistent workgroup per CU (registers)
+  hipLaunchKernelGGL(kfn, dim3(nwg), dim3(S::NT), S::LDS, st, dy, x, ws, H, W, tx, ty, (int)tiles);
+  return s3od_check_launch("conv3x3_wgrad_halo");
+}
+
 template <int BM, int BN> struct Tile {};
 
 // split-K factor of a wgrad GEMM from a time model: ceil(tiles*sp / slots) rounds of ceil(KT/sp)
@@ -518,6 +646,18 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
   ConvGeo g{}; g.B = B; g.SH = H; g.SW = W; g.SC = Cin; g.RH = OH; g.RW = OW; g.KH = KH; g.KW = KW; g.s = stride; g.p = pad;
   const int NPIX = B * OH * OW, M = Cout, N = KH * KW * Cin;
   hipStream_t st = (hipStream_t)stream;
+  static const int wg_knob = dev_knob("S3OD_WGRAD_HALO", 1);
+  if (wg_knob && dtype == S3OD_BF16 && ws && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && Cin == 64 &&
+      (Cout == 64 || Cout == 96)) {
+    (void)hipMemsetAsync(ws, 0, sizeof(float) * (size_t)M * N, st);
+    int rc = Cout == 64 ? (relu_x ? launch_wgrad_halo<64, true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, st)
+                                  : launch_wgrad_halo<64, false>((const bf16*)dy, (const bf16*)x, ws, B, H, W, st))
+                        : (relu_x ? launch_wgrad_halo<96, true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, st)
+                                  : launch_wgrad_halo<96, false>((const bf16*)dy, (const bf16*)x, ws, B, H, W, st));
+    if (rc) return rc;
+    hipLaunchKernelGGL(wgrad_permute_add_kernel, dim3(cdiv((long)M * N, 256)), dim3(256), 0, st, ws, dw, M, Cin, KH * KW);
+    return s3od_check_launch("conv_wgrad permute");
+  }
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(NPIX, KT<T>::BK);
     auto go = [&](auto bm, auto rl) -> int {

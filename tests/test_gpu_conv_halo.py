@@ -82,3 +82,22 @@ def test_mask_heads_fwd_halo():
           b2, logits, hsave, stream())
     _close(logits, ref, 3e-2)
     _close(hsave.view(B, H, W, 32 * NM), _nhwc(h))
+
+
+@pytest.mark.parametrize("cout,B,H,W,relu", [(64, 2, 37, 45, False), (96, 1, 40, 70, False), (64, 3, 16, 33, True)])
+def test_conv_wgrad_halo(cout, B, H, W, relu):
+    """3x3 s1 weight gradient (halo-tile kernel for Cin 64 -> Cout 64 / 96) vs torch's conv2d_weight of
+    the same bf16 operands, accumulated into an existing gradient (+=)."""
+    from s3od_amd._lib import lib, stream
+    g = torch.Generator(device="cuda").manual_seed(cout + H)
+    dy = torch.randn(B, cout, H, W, device="cuda", generator=g).bfloat16()
+    x = torch.randn(B, 64, H, W, device="cuda", generator=g).bfloat16()
+    xin = F.relu(x.float()) if relu else x.float()
+    ref = torch.nn.grad.conv2d_weight(xin, (cout, 64, 3, 3), dy.float(), padding=1)
+    dw0 = torch.randn(cout, 64, 3, 3, device="cuda", generator=g)
+    dw = dw0.clone()
+    ws = torch.empty(cout * 9 * 64, device="cuda")
+    lib()("s3od_conv_wgrad", BF16, B, H, W, 64, H, W, cout, 3, 3, 1, 1, _nhwc(dy), _nhwc(x), int(relu), dw, ws, 0, stream())
+    torch.cuda.synchronize()
+    got = dw - dw0
+    assert float((got - ref).abs().max() / ref.abs().max()) < 2e-3, float((got - ref).abs().max() / ref.abs().max())

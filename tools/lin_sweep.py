@@ -84,6 +84,14 @@ def dgrad_conv(name, B, H, Cin, Cout, k=3):
     report(name, 2.0 * B * H * H * Cout * Cin * k * k, timeit(f))
 
 
+def wgrad_conv(name, B, H, Cin, Cout):
+    dy, x = r(B, H, H, Cout), r(B, H, H, Cin)
+    dw = torch.zeros(Cout * 9 * Cin, device="cuda")
+    ws = torch.empty(Cout * 9 * Cin, device="cuda")
+    f = lambda: lib()("s3od_conv_wgrad", BF16, B, H, H, Cin, H, H, Cout, 3, 3, 1, 1, dy, x, 0, dw, ws, 0, stream())
+    report(name, 2.0 * B * H * H * Cout * Cin * 9, timeit(f))
+
+
 def heads(name, B, H):
     feat, w1 = r(B, H, H, 64), r(96, 3, 3, 64)
     b1, w2, b2 = r(96, dt=torch.float32), r(3, 32, dt=torch.float32), r(3, dt=torch.float32)
@@ -101,6 +109,8 @@ if __name__ == "__main__":
     if os.environ.get("SWEEP") == "conv64":
         conv("conv fwd 64->64 3x3 @1024^2 bs16 relu", 16, 1024, 64, 64, act=1)
         heads("mask heads fwd 64->96 (+relu+1x1) @1024^2 bs16", 16, 1024)
+        wgrad_conv("conv wgrad 64x(3x3x64) @1024^2 bs16", 16, 1024, 64, 64)
+        wgrad_conv("conv wgrad 96x(3x3x64) @1024^2 bs16", 16, 1024, 64, 96)
         dgrad_conv("conv dgrad 64<-64 3x3 @1024^2 bs16", 16, 1024, 64, 64)
         dgrad_conv("conv dgrad 64<-96 3x3 @1024^2 bs16", 16, 1024, 64, 96)
         sys.exit(0)
