@@ -328,15 +328,18 @@ template <class AT> DEV bf16x8 trf(const char* img, int r0, int col0, int lane, 
 template <int CO, bool RELU>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 conv3x3_wgrad_halo_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, float* __restrict__ ws, int H, int W,
-                          int tiles_x, int tiles_y, int ntiles) {
+                          int tiles_x, int tiles_y, int ntiles, int CinT, int CoT, int nci, int wpc) {
   typedef WgShape<CO> S;
   constexpr int NCO = CO / 16, CPD = CO / 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* dyi = smem;
   char* hxi = smem + S::DYB;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nwg = gridDim.x, xcd = blockIdx.x & 7, wpx = (nwg + 7 - xcd) >> 3, wi = blockIdx.x >> 3;
-  const int t_beg = (int)((long)ntiles * xcd / 8), t_end = (int)((long)ntiles * (xcd + 1) / 8);
+  // channel block of this workgroup: (co0 .. co0+CO) x (ci0 .. ci0+64) of a CoT x CinT conv; the wpc
+  // workgroups of one block split the tiles into contiguous ranges (neighbouring tiles share halo rows)
+  const int combo = blockIdx.x / wpc, wi = blockIdx.x - combo * wpc;
+  const int co0 = (combo / nci) * CO, ci0 = (combo % nci) * 64;
+  const int t_beg = (int)((long)ntiles * wi / wpc), t_end = (int)((long)ntiles * (wi + 1) / wpc);
   constexpr int NP = 9;                                  // (tap, ci-block) pairs of this wave: 9*wave ..
   const int pair0 = NP * wave;
   f32x4 acc[NP][NCO];
@@ -354,20 +357,20 @@ conv3x3_wgrad_halo_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ 
       pf[i] = make_uint4(0, 0, 0, 0);
       if (c < S::DCH) {                                   // dy tile: px = ty*32 + tx
         const int px = c / CPD, ch = c - px * CPD, gy = ty0 + px / HT_TW, gx = tx0 + px % HT_TW;
-        if (gy < H && gx < W) pf[i] = *(const uint4*)(dy + (((long)b * H + gy) * W + gx) * CO + ch * 8);
+        if (gy < H && gx < W) pf[i] = *(const uint4*)(dy + (((long)b * H + gy) * W + gx) * CoT + co0 + ch * 8);
       } else if (c < S::DCH + S::HCH) {                   // x halo
         const int c2 = c - S::DCH, px = c2 >> 3, ch = c2 & 7, hy = px / HT_HC, hx = px - hy * HT_HC;
         const int gy = ty0 - 1 + hy, gx = tx0 - 1 + hx;
         if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-          pf[i] = *(const uint4*)(x + (((long)b * H + gy) * W + gx) * 64 + ch * 8);
+          pf[i] = *(const uint4*)(x + (((long)b * H + gy) * W + gx) * CinT + ci0 + ch * 8);
           if (RELU) pf[i] = relu16<bf16>(pf[i]);
         }
       }
     }
   };
-  int tile = t_beg + wi;
+  int tile = t_beg;
   if (tile < t_end) prefetch(tile);
-  for (; tile < t_end; tile += wpx) {
+  for (; tile < t_end; tile++) {
 #pragma unroll
     for (int i = 0; i < S::PT; i++) {
       const int c = tid + S::NT * i;
@@ -375,7 +378,7 @@ conv3x3_wgrad_halo_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ 
       else if (c < S::DCH + S::HCH) { const int c2 = c - S::DCH; *(uint4*)(hxi + hx_at(c2 >> 3, (c2 & 7) * 16)) = pf[i]; }
     }
     __syncthreads();
-    if (tile + wpx < t_end) prefetch(tile + wpx);
+    if (tile + 1 < t_end) prefetch(tile + 1);
     for (int ty = 0; ty < HT_TH; ty++) {                  // K step = one output row of 32 pixels
       bf16x8 fa[NCO];
 #pragma unroll
@@ -398,12 +401,13 @@ conv3x3_wgrad_halo_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ 
 #pragma unroll
     for (int cb = 0; cb < NCO; cb++)
 #pragma unroll
-      for (int r = 0; r < 4; r++) atomicAdd(ws + (long)(cb * 16 + 4 * g + r) * 576 + tap * 64 + cib * 16 + li, acc[j][cb][r]);
+      for (int r = 0; r < 4; r++)
+        atomicAdd(ws + (long)(co0 + cb * 16 + 4 * g + r) * (9 * CinT) + tap * CinT + ci0 + cib * 16 + li, acc[j][cb][r]);
   }
 }
 
 template <int CO, bool RELU>
-static int launch_wgrad_halo(const bf16* dy, const bf16* x, float* ws, int B, int H, int W, hipStream_t st) {
+static int launch_wgrad_halo(const bf16* dy, const bf16* x, float* ws, int B, int H, int W, int CinT, int CoT, hipStream_t st) {
   typedef WgShape<CO> S;
   auto kfn = conv3x3_wgrad_halo_kernel<CO, RELU>;
   static bool attr = false;
@@ -412,8 +416,10 @@ static int launch_wgrad_halo(const bf16* dy, const bf16* x, float* ws, int B, in
   const long tiles = (long)B * tx * ty;
   static int ncu = 0;
   if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
-  const int nwg = (int)std::min<long>(tiles, (long)ncu);    // one persistent workgroup per CU (registers)
-  hipLaunchKernelGGL(kfn, dim3(nwg), dim3(S::NT), S::LDS, st, dy, x, ws, H, W, tx, ty, (int)tiles);
+  // one persistent workgroup per CU (registers) over all channel blocks: each block gets ~ncu/blocks of them
+  const int nci = CinT / 64, nblk = (CoT / CO) * nci;
+  const int wpc = (int)std::max<long>(1, std::min<long>(tiles, std::max(1, ncu / nblk)));
+  hipLaunchKernelGGL(kfn, dim3(nblk * wpc), dim3(S::NT), S::LDS, st, dy, x, ws, H, W, tx, ty, (int)tiles, CinT, CoT, nci, wpc);
   return s3od_check_launch("conv3x3_wgrad_halo");
 }
 
@@ -647,13 +653,17 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
   const int NPIX = B * OH * OW, M = Cout, N = KH * KW * Cin;
   hipStream_t st = (hipStream_t)stream;
   static const int wg_knob = dev_knob("S3OD_WGRAD_HALO", 1);
-  if (wg_knob && dtype == S3OD_BF16 && ws && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && Cin == 64 &&
-      (Cout == 64 || Cout == 96)) {
+  // halo-tile kernel: 3x3 s1 p1, Cin a multiple of 64, Cout a multiple of 64 (or 96 for the mask heads).
+  // Measured at bs 16 (tools/lin_sweep.py SWEEP=conv64): 2.4x / 1.75x on the 1024^2 64 -> 64 / 96 convs,
+  // 1.2x on 512^2 256 -> 128, equal at 256^2 / 128^2 and 8 % slower at 64^2 -> used for Cin 64 or >= 512^2 maps
+  const int coblk = Cout % 64 == 0 ? 64 : (Cout == 96 ? 96 : 0);
+  if (wg_knob && dtype == S3OD_BF16 && ws && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W &&
+      Cin % 64 == 0 && coblk && (Cin == 64 || (long)H * W >= 512L * 512)) {
     (void)hipMemsetAsync(ws, 0, sizeof(float) * (size_t)M * N, st);
-    int rc = Cout == 64 ? (relu_x ? launch_wgrad_halo<64, true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, st)
-                                  : launch_wgrad_halo<64, false>((const bf16*)dy, (const bf16*)x, ws, B, H, W, st))
-                        : (relu_x ? launch_wgrad_halo<96, true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, st)
-                                  : launch_wgrad_halo<96, false>((const bf16*)dy, (const bf16*)x, ws, B, H, W, st));
+    int rc = coblk == 64 ? (relu_x ? launch_wgrad_halo<64, true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)
+                                   : launch_wgrad_halo<64, false>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st))
+                         : (relu_x ? launch_wgrad_halo<96, true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)
+                                   : launch_wgrad_halo<96, false>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st));
     if (rc) return rc;
     hipLaunchKernelGGL(wgrad_permute_add_kernel, dim3(cdiv((long)M * N, 256)), dim3(256), 0, st, ws, dw, M, Cin, KH * KW);
     return s3od_check_launch("conv_wgrad permute");

@@ -101,3 +101,20 @@ def test_conv_wgrad_halo(cout, B, H, W, relu):
     torch.cuda.synchronize()
     got = dw - dw0
     assert float((got - ref).abs().max() / ref.abs().max()) < 2e-3, float((got - ref).abs().max() / ref.abs().max())
+
+
+@pytest.mark.parametrize("cin,cout,B,H,W,relu", [(256, 256, 2, 20, 36, True), (128, 192, 1, 17, 40, False),
+                                                  (512, 256, 1, 9, 12, False)])
+def test_conv_wgrad_halo_channel_blocks(cin, cout, B, H, W, relu):
+    """The halo wgrad over 64-channel blocks of wider convs (the RCU / layer_rn / output_conv shapes)."""
+    from s3od_amd._lib import lib, stream
+    g = torch.Generator(device="cuda").manual_seed(cin + cout)
+    dy = torch.randn(B, cout, H, W, device="cuda", generator=g).bfloat16()
+    x = torch.randn(B, cin, H, W, device="cuda", generator=g).bfloat16()
+    xin = F.relu(x.float()) if relu else x.float()
+    ref = torch.nn.grad.conv2d_weight(xin, (cout, cin, 3, 3), dy.float(), padding=1)
+    dw = torch.zeros(cout, cin, 3, 3, device="cuda")
+    ws = torch.empty(cout * 9 * cin, device="cuda")
+    lib()("s3od_conv_wgrad", BF16, B, H, W, cin, H, W, cout, 3, 3, 1, 1, _nhwc(dy), _nhwc(x), int(relu), dw, ws, 0, stream())
+    torch.cuda.synchronize()
+    assert float((dw - ref).abs().max() / ref.abs().max()) < 2e-3, float((dw - ref).abs().max() / ref.abs().max())

@@ -111,6 +111,11 @@ if __name__ == "__main__":
         heads("mask heads fwd 64->96 (+relu+1x1) @1024^2 bs16", 16, 1024)
         wgrad_conv("conv wgrad 64x(3x3x64) @1024^2 bs16", 16, 1024, 64, 64)
         wgrad_conv("conv wgrad 96x(3x3x64) @1024^2 bs16", 16, 1024, 64, 96)
+        wgrad_conv("conv wgrad 256x(3x3x256) @256^2 bs16", 16, 256, 256, 256)
+        wgrad_conv("conv wgrad 128x(3x3x256) @512^2 bs16", 16, 512, 256, 128)
+        wgrad_conv("conv wgrad 256x(3x3x256) @128^2 bs16", 16, 128, 256, 256)
+        wgrad_conv("conv wgrad 256x(3x3x1024) @64^2 bs16", 16, 64, 1024, 256)
+        wgrad_conv("conv wgrad 256x(3x3x256) @64^2 bs16", 16, 64, 256, 256)
         dgrad_conv("conv dgrad 64<-64 3x3 @1024^2 bs16", 16, 1024, 64, 64)
         dgrad_conv("conv dgrad 64<-96 3x3 @1024^2 bs16", 16, 1024, 64, 96)
         sys.exit(0)
