@@ -20,6 +20,7 @@
 // block-level functor (bias / BN-fold / activation / residual / RoPE / atomics ...).
 #pragma once
 #include "common.hpp"
+#include <algorithm>
 
 constexpr int GEMM_THREADS = 512;          // 8 waves per workgroup (2 per SIMD)
 constexpr int GEMM_WAVES = GEMM_THREADS / 64;
@@ -160,6 +161,7 @@ template <typename T, int R, int NW = GEMM_WAVES> struct MCGeom {
 };
 
 template <typename T, int R, int NW = GEMM_WAVES> struct DenseKC {          // X[row*ld + k]
+  static constexpr int ROWS = R;
   static constexpr bool KCL = true, RELU = false;
   typedef KCGeom<T, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* p; long ld; int nrows, K; int relu;
@@ -202,6 +204,7 @@ template <typename T, int R, int NW = GEMM_WAVES> struct DenseKC {          // X
 };
 
 template <typename T, int R, int NW = GEMM_WAVES> struct DenseMC {          // X[k*ld + col]
+  static constexpr int ROWS = R;
   static constexpr bool KCL = false, RELU = false;
   typedef MCGeom<T, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* p; long ld; int K, ncols;
@@ -278,6 +281,7 @@ struct TapWalk {
 
 // conv forward A operand: rows = output pixels (b,oy,ox) of RH x RW, k = tap*SC + c
 template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct ConvFwdA {
+  static constexpr int ROWS = R;
   static constexpr bool KCL = true, RELU = RELU_;
   typedef KCGeom<T, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* x; ConvGeo g; int M; int relu;
@@ -351,6 +355,7 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Con
 
 // dgrad / ConvT A operand: rows = class pixels (b, y', x'), k = (jh*ntw + jw)*SC + c
 template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradA {
+  static constexpr int ROWS = R;
   static constexpr bool KCL = true, RELU = false;
   typedef KCGeom<T, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* dy; ConvGeo g; int M;
@@ -425,6 +430,7 @@ template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradA {
 
 // dgrad / ConvT B operand (MC): B[k=(jh,jw,c)][n] = W[c][kh0+s*jh][kw0+s*jw][n], W repacked [C][KH][KW][N]
 template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradB {
+  static constexpr int ROWS = R;
   static constexpr bool KCL = false, RELU = false;
   typedef MCGeom<T, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* w; ConvGeo g; int NC;     // NC = output channels of the dgrad (= conv input channels)
@@ -483,6 +489,7 @@ template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradB {
 // Fast path (RW % BK == 0): the 64 pixels of a K tile share one output row, so (b, oy, ox0) are
 // wave-uniform and interior tiles need no per-lane bounds test.
 template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct WgradB {
+  static constexpr int ROWS = R;
   static constexpr bool KCL = false, RELU = RELU_;
   typedef MCGeom<T, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
   const T* x; ConvGeo g; int NPIX; int relu;   // g.SC = Cin of X, g.SH/SW = X dims, RH/RW = output grid
@@ -758,12 +765,12 @@ __global__ void __launch_bounds__(GEMM_THREADS) igemm_kernel(LA la, LB lb, EPI e
       cur = nxt;
     }
   }
-  __syncthreads();
+  lds_barrier();
   // stage the C tile to LDS (fp32) in row chunks of CROWS and hand each chunk to the epilogue
   float* ct = (float*)smem;
 #pragma unroll
   for (int c0 = 0; c0 < BM; c0 += S::CROWS) {
-    if (c0) __syncthreads();
+    if (c0) lds_barrier();
 #pragma unroll
     for (int i = 0; i < MI; i++) {
       const int rb = wm * S::TM + i * 16;                    // wave-uniform
@@ -775,7 +782,7 @@ __global__ void __launch_bounds__(GEMM_THREADS) igemm_kernel(LA la, LB lb, EPI e
         *(float4*)(ct + r * S::LDT + c) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
       }
     }
-    __syncthreads();
+    lds_barrier();
     epi(ct, S::LDT, m0 + c0, n0, tid, S::CROWS, BN, GEMM_THREADS);
   }
 }
@@ -908,11 +915,11 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
     }
     if (csum) {
       // reduce the per-thread 8-column partials over the row phases through the (consumed) C tile
-      __syncthreads();
+      lds_barrier();
       float* red = (float*)ct;
 #pragma unroll
       for (int e = 0; e < 8; e++) red[tid * 8 + e] = cs8[e];
-      __syncthreads();
+      lds_barrier();
       const int spr = BN / 8, nph = NT / spr;
       if (tid < BN && n0 + tid < N) {
         const int g = tid >> 3, e = tid & 7;
@@ -942,14 +949,199 @@ struct EpiWgrad {
   }
 };
 
+// ------------------------------------------------------------------ 256x256 ping-pong kernel (bf16)
+// 8 waves = 2 (M) x 4 (N), each owning a 128x64 sub-tile (acc[8][4], 128 VGPRs); waves w and w+4
+// share a SIMD (cyclic wave->SIMD placement), so the two M halves are SIMD partners.  The M half
+// wr = 1 runs one barrier behind wr = 0: while one wave of a SIMD runs its 16-MFMA block, its
+// partner issues the next block's LDS reads and LDS-DMA (MI355X_MICROARCH.md "Two waves per SIMD",
+// cdna_hip_programming.md §5 "256² 8-phase template").
+//
+// Each K tile (BK = 64) is 4 phases = the wave's 4 C quadrants (64 rows x 32 cols) in the order
+// (0,0) (0,1) (1,1) (1,0); a phase is  [LDS reads | DMA issue] barrier [16 MFMA] barrier.  All of a
+// tile's fragments are read in its phases 0 and 1 (A0+B0, then B1+A1: 96 VGPRs), so its LDS buffer
+// is free from phase 3 on and the DMA of tile t+2 can start there, a whole tile ahead.
+// LDS: 2 buffers x 4 half images (A rows 0-127 / 128-255, B cols 0-127 / 128-255; 16 KB each), so
+// the loaders run with R = 128.  Tile t+1's A halves are issued in phase 3 of tile t-1 and its B
+// halves in phase 0 of tile t; phase 3 of tile t retires both with a counted vmcnt.
+//   RAW: every wave's wait for tile t+1 sits in its phase-3 load segment of tile t, i.e. before the
+//        barrier that precedes the first read of tile t+1 by either stagger half;
+//   WAR: a buffer's last reads are in phase 1; it is restaged in phase 3 (>= 2 phases later, so
+//        every reader's lgkmcnt(0) precedes a barrier the restaging wave has passed).
+// Fragment addressing inside a 128-row half image with every read's row0 a multiple of 16: the
+// per-lane part of the address is computed once and the row0 / kk parts become immediates.
+//   KC [128][128 B]: kc_off(row0 + l, b) = row0*128 + kc_off(l, b)   ((r>>1)&7 depends on l only)
+//   MC [64 k][256 B]: mc_off<256>(kk*32 + 8g + q, 2*row0 + 8p)
+//                     = kk*8192 + (8g+q)*256 + 8p + (((row0>>4) ^ gk) << 5),  gk = q | (g&1)<<2
+template <bool KCL> struct PPFrag;
+template <> struct PPFrag<true> {
+  int o[2];
+  DEV void init(int lane, int) {
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++) o[kk] = kc_off(lane & 15, kk * 64 + (lane >> 4) * 16);
+  }
+  DEV bf16x8 read(const char* img, int row0, int kk) const { return *(const bf16x8*)(img + o[kk] + row0 * 128); }
+};
+template <> struct PPFrag<false> {
+  int base, gk;
+  // h64: the reads' rows are offset by 64 * h64 (folded into the XOR: (4 h64 | m) ^ gk = m ^ (gk ^ 4 h64))
+  DEV void init(int lane, int h64) {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    base = (8 * g + q) * 256 + 8 * p; gk = (q | ((g & 1) << 2)) ^ (h64 << 2);
+  }
+  DEV bf16x8 read(const char* img, int row0, int kk) const {
+    typedef __attribute__((address_space(3))) s16x4 lds_s4;
+    const char* a = img + base + ((((row0 >> 4) ^ gk)) << 5) + kk * 8192;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)a);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(a + 1024));
+    bf16x4 x = __builtin_bit_cast(bf16x4, lo), y = __builtin_bit_cast(bf16x4, hi);
+    bf16x8 r;
+    r[0] = x[0]; r[1] = x[1]; r[2] = x[2]; r[3] = x[3]; r[4] = y[0]; r[5] = y[1]; r[6] = y[2]; r[7] = y[3];
+    return r;
+  }
+};
+
+DEV void raw_barrier() { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); }
+
+// The epilogue stages C through the K-stage LDS in two 128-row chunks with LDS barriers only (a
+// __syncthreads() would drain the stores).  (A persistent variant -- the next tile's first K
+// stage issued behind this tile's stores -- measured within 5 % of this at 20 spilled VGPRs.)
+template <class LA, class LB, class EPI>
+__global__ void __launch_bounds__(GEMM_THREADS, 1) igemm_pp_kernel(LA la0, LB lb0, EPI epi, int KTILES, int split, int flags) {
+  typedef bf16 T;
+  constexpr int BM = 256, BN = 256, HB = 128 * 128, STG = 4 * HB, LDT = BN + 4;
+  static_assert(sizeof(T) == 2 && KT<T>::BK == 64, "ping-pong kernel is bf16 only");
+  static_assert(128 * LDT * 4 <= 160 * 1024 && 2 * STG <= 128 * LDT * 4, "ping-pong LDS budget");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int wr = wave >> 2, wc = wave & 3;
+  int m0, n0;
+  {
+    const int nwg = gridDim.x * gridDim.y;
+    const int L = blockIdx.y * gridDim.x + blockIdx.x;
+    const int q = nwg >> 3, r = nwg & 7, xcd = L & 7, idx = L >> 3;
+    const int W = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+    m0 = (W / gridDim.x) * BM; n0 = (W % gridDim.x) * BN;
+  }
+  const int per = (KTILES + split - 1) / split;
+  const int kt0 = blockIdx.z * per, kt1 = min(KTILES, kt0 + per);
+  const int nt = kt1 - kt0;
+  epi.prepare(blockIdx.z);
+  LA la1 = la0; LB lb1 = lb0;
+  la0.setup(m0, tid); la1.setup(m0 + 128, tid);
+  lb0.setup(n0, tid); lb1.setup(n0 + 128, tid);
+  constexpr int NA = LA::NIW * 2;              // DMA instructions per wave for the two A halves
+  const bool stag = !(flags & 1);              // dev knob S3OD_PP_FLAGS bit 0: no stagger
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nt > 0) {
+    // first K stage: buffer 0 whole + buffer 1's A halves
+    la0.issue(kt0, smem); la1.issue(kt0, smem + HB); lb0.issue(kt0, smem + 2 * HB); lb1.issue(kt0, smem + 3 * HB);
+    if (nt > 1) { la0.issue(kt0 + 1, smem + STG); la1.issue(kt0 + 1, smem + STG + HB); wait_vmcnt<NA>(); }
+    else wait_vmcnt<0>();
+    raw_barrier();
+    if (wr && stag) raw_barrier();             // stagger: the wr = 1 half runs one barrier behind
+    PPFrag<LA::KCL> pfa; pfa.init(lane, 0);
+    PPFrag<LB::KCL> pfb; pfb.init(lane, wc & 1);                        // this wave's 64 B columns
+    const int boff = LB::KCL ? (wc & 1) * 64 * 128 : 0;
+    bf16x8 fa[2][4][2], fb[2][2][2];
+    auto rdA = [&](const char* As, int qm) {
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++) {
+          fa[qm][i][kk] = pfa.read(As, qm * 64 + i * 16, kk);
+          if constexpr (LA::RELU) fa[qm][i][kk] = relu_frag(fa[qm][i][kk]);
+        }
+    };
+    auto rdB = [&](const char* Bs, int qn) {
+#pragma unroll
+      for (int j = 0; j < 2; j++)
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++) {
+          fb[qn][j][kk] = pfb.read(Bs, qn * 32 + j * 16, kk);
+          if constexpr (LB::RELU) fb[qn][j][kk] = relu_frag(fb[qn][j][kk]);
+        }
+    };
+    auto mm = [&](int qm, int qn) {
+      raw_barrier();
+      wait_lgkm0();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+          for (int j = 0; j < 2; j++)
+            acc[qm * 4 + i][qn * 2 + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[qn][j][kk], fa[qm][i][kk], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      raw_barrier();
+    };
+    for (int t = 0; t < nt; ++t) {
+      char* cb = smem + (t & 1) * STG;
+      char* nb = smem + ((t + 1) & 1) * STG;
+      const char* As = cb + wr * HB;
+      const char* Bs = cb + (2 + (wc >> 1)) * HB + boff;
+      // phase 0: quadrant (0,0); B halves of tile t+1
+      rdA(As, 0); rdB(Bs, 0);
+      if (t + 1 < nt) { lb0.issue(kt0 + t + 1, nb + 2 * HB); lb1.issue(kt0 + t + 1, nb + 3 * HB); }
+      mm(0, 0);
+      // phase 1: quadrant (0,1); the tile's last LDS reads
+      rdB(Bs, 1); rdA(As, 1);
+      mm(0, 1);
+      // phase 2: quadrant (1,1)
+      mm(1, 1);
+      // phase 3: quadrant (1,0); A halves of tile t+2 into this tile's buffer; retire tile t+1
+      if (t + 2 < nt) { la0.issue(kt0 + t + 2, cb); la1.issue(kt0 + t + 2, cb + HB); wait_vmcnt<NA>(); }
+      else if (t + 1 < nt) wait_vmcnt<0>();
+      mm(1, 0);
+    }
+    if (!wr && stag) raw_barrier();            // re-align the two halves
+  }
+  float* ct = (float*)smem;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    lds_barrier();
+    if (wr == h) {
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int r = i * 16 + (lane & 15), col = wc * 64 + j * 16 + (lane >> 4) * 4;
+          *(f32x4*)(ct + r * LDT + col) = acc[i][j];
+        }
+    }
+    lds_barrier();
+    epi(ct, LDT, m0 + h * 128, n0, tid, 128, BN, GEMM_THREADS);
+  }
+}
+constexpr int PP_LDS = 128 * (256 + 4) * 4;   // C chunk (133 KB) >= the two 64 KB K stages
+
 // WM_: waves along M (0 = by tile shape); e.g. 512x64 tiles use WM_=8 for 64x64 per-wave tiles
 template <typename T, int BM, int BN, class LA, class LB, class EPI, int NST = 3, int WM_ = 0>
 static int launch_igemm(LA la, LB lb, EPI epi, int M, int N, int KTILES, int split, int zdim_extra, hipStream_t st) {
-  if (!la.buf_ok() || !lb.buf_ok()) {
-    s3od_set_error("igemm: operand window too large for a buffer descriptor or gather channels < %d", KT<T>::BK / 2);
-    return 22;
-  }
-  {
+  if constexpr (LA::ROWS * 2 == BM) {           // half-row loaders: the 256x256 ping-pong kernel
+    static_assert(BM == 256 && BN == 256 && LB::ROWS == 128 && sizeof(T) == 2, "ping-pong config");
+    if (!la.buf_ok() || !lb.buf_ok()) {
+      s3od_set_error("igemm: operand window too large for a buffer descriptor or gather channels < %d", KT<T>::BK / 2);
+      return 22;
+    }
+    auto kfn = igemm_pp_kernel<LA, LB, EPI>;
+    static bool attr = false;
+    if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS); attr = true; }
+    static const int flags = dev_knob("S3OD_PP_FLAGS", 0);
+    dim3 grid(cdiv(N, BN), cdiv(M, BM), split * zdim_extra);
+    hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), PP_LDS, st, la, lb, epi, KTILES, split, flags);
+    return s3od_check_launch("igemm_pp");
+  } else {
+    if (!la.buf_ok() || !lb.buf_ok()) {
+      s3od_set_error("igemm: operand window too large for a buffer descriptor or gather channels < %d", KT<T>::BK / 2);
+      return 22;
+    }
     typedef GemmShape<T, BM, BN, NST, WM_> S;
     auto kfn = igemm_kernel<T, BM, BN, NST, LA, LB, EPI, WM_>;
     static bool attr = false;

@@ -1,6 +1,7 @@
 // C-ABI entry points built on the implicit-GEMM engine (gemm.hpp).
 #include "gemm.hpp"
 #include <type_traits>
+#include <utility>
 
 #define DISPATCH_T(dtype, ...)                                                  \
   do {                                                                          \
@@ -23,17 +24,39 @@ static int gemm_cfg() {
   return c;
 }
 // W = waves that issue the operand loads (the loaders are built for that many waves)
-template <int BM_, int BN_, int NST_, int W_ = GEMM_WAVES, int WM_ = 0> struct TileCfg {
+// PP_: the 256x256 ping-pong kernel (bf16 only), whose loaders stage half tiles (LM / LN rows)
+template <int BM_, int BN_, int NST_, int W_ = GEMM_WAVES, int WM_ = 0, bool PP_ = false> struct TileCfg {
   static constexpr int BM = BM_, BN = BN_, NST = NST_, W = W_, WM = WM_;
+  static constexpr bool PP = PP_;
+  static constexpr int LM = PP_ ? BM_ / 2 : BM_, LN = PP_ ? BN_ / 2 : BN_;
 };
+// a conv whose output-channel tile is narrower than 256 cannot run the ping-pong kernel
+template <class C, int BNW> using ConvCfg = std::conditional_t<(C::PP && BNW < 256), TileCfg<128, 128, 2>, C>;
 // call f(TileCfg) for the selected config; `def` = per-op default config index
+// the M-tail launches (below) force the 128x128 config through this override
+static thread_local int tl_cfg = -1;
+struct TailCfg {
+  int saved;
+  TailCfg() : saved(tl_cfg) { tl_cfg = 1; }
+  ~TailCfg() { tl_cfg = saved; }
+};
+// M tail: rows past the last full 256-row panel (M = 16 * 4101 = 65616 leaves 80) would cost a whole
+// extra round of full-K tiles (e.g. o_proj 3078 tiles on 512 slots = 7 rounds, 6 without the tail);
+// they run as a second, small launch on 128x128 tiles instead.  Dev knob S3OD_M_TAIL=0 disables.
+static bool split_tail(int M) {
+  static const int knob = dev_knob("S3OD_M_TAIL", 1);
+  return knob && tl_cfg < 0 && M > 256 && (M & 255) != 0;
+}
 template <typename T, class F> static int with_cfg(int def, F f) {
-  int c = gemm_cfg(); if (c < 0) c = def;
+  int c = tl_cfg >= 0 ? tl_cfg : gemm_cfg(); if (c < 0) c = def;
   switch (c) {
     case 1: return f(TileCfg<128, 128, 2>{});
     case 2: return f(TileCfg<128, 128, 3>{});
     case 3: return f(TileCfg<256, 128, 2>{});
     case 4: return f(TileCfg<256, 256, 2>{});
+    case 5:
+      if constexpr (sizeof(T) == 2) return f(TileCfg<256, 256, 2, GEMM_WAVES, 0, true>{});
+      else return f(TileCfg<128, 128, 2>{});
     default: return f(TileCfg<256, 128, 3>{});
   }
 }
@@ -44,6 +67,7 @@ template <typename T, class F> static int with_cfg(int def, F f) {
 template <typename T> struct EpiQKV {
   T* q; T* k; T* v; const float* bias; const float* cs; const float* sn;
   int M, Ntok, P, H;
+  int moff = 0;                       // global token row of local row 0 (M-tail launch)
   DEV void prepare(int) {}
   DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN, int NT) const {
     // this thread's fixed 8-column group: bias of its columns and of their RoPE partners (d +- 32)
@@ -56,7 +80,7 @@ template <typename T> struct EpiQKV {
     const bool fixed_cols = NT % (BN / 8) == 0;
     for_segments(ct, LDT, BM, BN, m0, n0, M, 3 * H * 64, tid, NT, [&](int m, int n, const float* a, int r, int c) {
       int which = n / (H * 64), nn = n - which * H * 64, h = nn >> 6, d0 = nn & 63;
-      int b = m / Ntok, t = m - b * Ntok;
+      int b = (m + moff) / Ntok, t = (m + moff) - b * Ntok;
       float val[8];
 #pragma unroll
       for (int e = 0; e < 8; e++) val[e] = a[e] + (fixed_cols ? b8[e] : (bias ? bias[n + e] : 0.f));
@@ -464,19 +488,34 @@ int s3od_linear_fwd(int dtype, int M, int N, int K, const void* x, long ldx, con
                     void* out, long ldo, int out_f32, void* pre, long ldp,
                     int row_mode, int P, int prefix, void* stream) {
   S3OD_REQUIRE(K % 8 == 0 && N % 8 == 0, "linear_fwd: K and N must be multiples of 8 (K=%d N=%d)", K, N);
+  if (row_mode == 0 && split_tail(M)) {
+    const int M1 = M & ~255, M2 = M - M1;
+    int rc = s3od_linear_fwd(dtype, M1, N, K, x, ldx, w, bias, scale, shift, act, res1, ldr1, res2, ldr2, res_f32,
+                             out, ldo, out_f32, pre, ldp, row_mode, P, prefix, stream);
+    if (rc) return rc;
+    const long es = dtype == S3OD_BF16 ? 2 : 4, eo = out_f32 ? 4 : es, er = res_f32 ? 4 : es;
+    TailCfg tail;
+    return s3od_linear_fwd(dtype, M2, N, K, (const char*)x + M1 * ldx * es, ldx, w, bias, scale, shift, act,
+                           res1 ? (const char*)res1 + M1 * ldr1 * er : nullptr, ldr1,
+                           res2 ? (const char*)res2 + M1 * ldr2 * er : nullptr, ldr2, res_f32,
+                           (char*)out + M1 * ldo * eo, ldo, out_f32, pre ? (char*)pre + M1 * ldp * es : nullptr, ldp,
+                           row_mode, P, prefix, stream);
+  }
   RowMap rm = dense_rm(); rm.mode = row_mode; rm.P = P; rm.prefix = prefix;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(K, KT<T>::BK);
     auto go = [&](auto tile, auto tout, auto tres) -> int {
       typedef decltype(tout) TO; typedef decltype(tres) TR;
-      // measured (tools/lin_sweep.py): 256x128 x 3 stages for K >= 2048; the GELU(+pre) up-projection
-      // runs best on 256x256 tiles (574 vs 621 us at M=65616 N=3072 K=768); 128x128 otherwise
-      const int def = K >= 2048 ? 0 : (act == ACT_GELU && N >= 2048 ? 4 : 1);
+      // measured (tools/lin_sweep.py, bs 16 1024^2): the 256x256 ping-pong kernel for the large ViT
+      // linears (o_proj 241 -> 215 us, up 576 -> 563, down 487 -> 418); else 256x128 x 3 stages for
+      // K >= 2048, 256x256 for the GELU up-projection, 128x128 otherwise
+      const int def = (M >= 16384 && N >= 768 && N % 256 == 0) ? 5
+                      : (K >= 2048 ? 0 : (act == ACT_GELU && N >= 2048 ? 4 : 1));
       return with_cfg<T>(def, [&](auto C) -> int {
         constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
-        DenseKC<T, BM, decltype(C)::W> la{(const T*)x, ldx, M, K, 0};
-        DenseKC<T, BN, decltype(C)::W> lb{(const T*)w, (long)K, N, K, 0};
+        DenseKC<T, decltype(C)::LM, decltype(C)::W> la{(const T*)x, ldx, M, K, 0};
+        DenseKC<T, decltype(C)::LN, decltype(C)::W> lb{(const T*)w, (long)K, N, K, 0};
         EpiStd<TO, TR, T> e{(TO*)out, ldo, 0, bias, scale, shift, (const TR*)res1, ldr1, (const TR*)res2, ldr2,
                             (T*)pre, ldp, nullptr, act, M, N, rm};
         static const int epi_probe = dev_knob("S3OD_EPI_PROBE", 0);   // dev: 1 = skip the epilogue's stores
@@ -498,14 +537,27 @@ int s3od_linear_dgrad(int dtype, int M, int N, int K, const void* dy, long lddy,
                       int act, const void* aux, long ldaux, void* dx, long lddx, int out_f32,
                       int row_mode, int P, int prefix, float* colsum, void* stream) {
   S3OD_REQUIRE(K % 8 == 0 && N % 8 == 0, "linear_dgrad: K,N %% 8");
+  if (row_mode == 0 && split_tail(M)) {
+    const int M1 = M & ~255, M2 = M - M1;
+    int rc = s3od_linear_dgrad(dtype, M1, N, K, dy, lddy, w, act, aux, ldaux, dx, lddx, out_f32, row_mode, P, prefix,
+                               colsum, stream);
+    if (rc) return rc;
+    const long es = dtype == S3OD_BF16 ? 2 : 4, eo = out_f32 ? 4 : es;
+    TailCfg tail;
+    return s3od_linear_dgrad(dtype, M2, N, K, (const char*)dy + M1 * lddy * es, lddy, w, act,
+                             aux ? (const char*)aux + M1 * ldaux * eo : nullptr, ldaux, (char*)dx + M1 * lddx * eo, lddx,
+                             out_f32, row_mode, P, prefix, colsum, stream);
+  }
   RowMap rm = dense_rm(); rm.mode = row_mode; rm.P = P; rm.prefix = prefix;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(K, KT<T>::BK);
-    return with_cfg<T>(1, [&](auto C) -> int {
+    // ping-pong 256x256 for the long-K dgrads (up 441 -> 374 us, qkv 334 -> 292); 128x128 for K = 768
+    const int def = (M >= 16384 && K >= 2048 && N % 256 == 0) ? 5 : 1;
+    return with_cfg<T>(def, [&](auto C) -> int {
       constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
-      DenseKC<T, BM, decltype(C)::W> la{(const T*)dy, lddy, M, K, 0};
-      DenseMC<T, BN, decltype(C)::W> lb{(const T*)w, (long)N, K, N};
+      DenseKC<T, decltype(C)::LM, decltype(C)::W> la{(const T*)dy, lddy, M, K, 0};
+      DenseMC<T, decltype(C)::LN, decltype(C)::W> lb{(const T*)w, (long)N, K, N};
       if (out_f32) {
         // f32 output: aux is an f32 tensor to add (e.g. the residual-stream gradient, in place)
         EpiStd<float, float> e{(float*)dx, lddx, 0, nullptr, nullptr, nullptr, (const float*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, rm, colsum};
@@ -525,14 +577,14 @@ int s3od_linear_wgrad(int dtype, int Nout, int Kin, int rows, const void* dy, lo
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(rows, KT<T>::BK);
-    // measured (tools/lin_sweep.py, bs16 1024^2 ViT shapes): 128x128 tiles for the large outputs
-    // (3072x768, 2304x768, 768x3072: 7-12 % faster than 256x256), 256x128 for 768x768
-    const int def = (long)Nout * Kin <= 1024L * 1024 ? 0 : 1;
+    // measured (tools/lin_sweep.py, bs16 1024^2 ViT shapes): the 256x256 ping-pong kernel for the large
+    // outputs (3072x768 441 -> 403 us, 768x3072 457 -> 398, 2304x768 335 -> 308), 256x128 for 768x768
+    const int def = (long)Nout * Kin <= 1024L * 1024 ? 0 : 5;
     return with_cfg<T>(def, [&](auto C) -> int {
       constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
       int sp = split > 0 ? split : wgrad_split<T, BM, BN, NST>(cdiv(Nout, BM) * cdiv(Kin, BN), KTILES);
-      DenseMC<T, BM, decltype(C)::W> la{(const T*)dy, lddy, rows, Nout};
-      DenseMC<T, BN, decltype(C)::W> lb{(const T*)x, ldx, rows, Kin};
+      DenseMC<T, decltype(C)::LM, decltype(C)::W> la{(const T*)dy, lddy, rows, Nout};
+      DenseMC<T, decltype(C)::LN, decltype(C)::W> lb{(const T*)x, ldx, rows, Kin};
       EpiWgrad e{dw, Nout, Kin, Kin, 1};
       return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, Nout, Kin, KTILES, sp, 1, st);
     });
@@ -543,16 +595,25 @@ int s3od_linear_wgrad(int dtype, int Nout, int Kin, int rows, const void* dy, lo
 // fused QKV projection + bias + RoPE + head split. x: [B*Ntok, D] T ; w: [3D, D] T ; D = 64 H
 int s3od_qkv_rope_fwd(int dtype, int B, int Ntok, int P, int H, const void* x, const void* w, const float* bias,
                       const float* cos_t, const float* sin_t, void* q, void* k, void* v, void* stream) {
-  const int D = 64 * H, N = 3 * D, M = B * Ntok;
+  const int D = 64 * H, N = 3 * D, Mall = B * Ntok;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
-    return with_cfg<T>(4, [&](auto C) -> int {
-      constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
-      DenseKC<T, BM, decltype(C)::W> la{(const T*)x, (long)D, M, D, 0};
-      DenseKC<T, BN, decltype(C)::W> lb{(const T*)w, (long)D, N, D, 0};
-      EpiQKV<T> e{(T*)q, (T*)k, (T*)v, bias, cos_t, sin_t, M, Ntok, P, H};
-      return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, M, N, cdiv(D, KT<T>::BK), 1, 1, st);
-    });
+    auto part = [&](int m_first, int M) -> int {
+      return with_cfg<T>(5, [&](auto C) -> int {
+        constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
+        DenseKC<T, decltype(C)::LM, decltype(C)::W> la{(const T*)x + (long)m_first * D, (long)D, M, D, 0};
+        DenseKC<T, decltype(C)::LN, decltype(C)::W> lb{(const T*)w, (long)D, N, D, 0};
+        EpiQKV<T> e{(T*)q, (T*)k, (T*)v, bias, cos_t, sin_t, M, Ntok, P, H};
+        e.moff = m_first;
+        return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, M, N, cdiv(D, KT<T>::BK), 1, 1, st);
+      });
+    };
+    if (!split_tail(Mall)) return part(0, Mall);
+    const int M1 = Mall & ~255;
+    int rc = part(0, M1);
+    if (rc) return rc;
+    TailCfg tail;
+    return part(M1, Mall - M1);
   });
   return 0;
 }
@@ -579,11 +640,14 @@ int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int C
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(K, KT<T>::BK);
     auto go = [&](auto bn, auto rl) -> int {
-      return with_cfg<T>(Cout <= 64 ? 3 : 1, [&](auto C) -> int {
-        constexpr int BM = decltype(C)::BM, NST = decltype(C)::NST;
-        constexpr int BN = decltype(bn)::value < decltype(C)::BN ? decltype(bn)::value : decltype(C)::BN;
-        ConvFwdA<T, BM, decltype(rl)::value, decltype(C)::W> la{}; la.x = (const T*)x; la.g = g; la.M = M; la.relu = relu_in;
-        DenseKC<T, BN, decltype(C)::W> lb{(const T*)wp, (long)K, N, K, 0};
+      return with_cfg<T>(Cout <= 64 ? 3 : 1, [&](auto C0) -> int {
+        typedef ConvCfg<decltype(C0), decltype(bn)::value> CC;
+        constexpr int BM = CC::BM, NST = CC::NST;
+        constexpr int BN = decltype(bn)::value < CC::BN ? decltype(bn)::value : CC::BN;
+        constexpr int LN = CC::PP ? CC::LN : BN;
+        CC C{};
+        ConvFwdA<T, CC::LM, decltype(rl)::value, CC::W> la{}; la.x = (const T*)x; la.g = g; la.M = M; la.relu = relu_in;
+        DenseKC<T, LN, CC::W> lb{(const T*)wp, (long)K, N, K, 0};
         EpiStd<T, T> e{(T*)out, (long)Cout, 0, bias, scale, shift, (const T*)res1, (long)Cout, (const T*)res2, (long)Cout,
                        (T*)pre, (long)Cout, stats, act, M, N, dense_rm(), colsum};
         return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, M, N, KTILES, 1, 1, st);
@@ -591,10 +655,12 @@ int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int C
     };
     if (relu_in) {
       if (Cout <= 64) return go(std::integral_constant<int, 64>{}, std::true_type{});
-      return go(std::integral_constant<int, 128>{}, std::true_type{});
+      if (Cout < 256) return go(std::integral_constant<int, 128>{}, std::true_type{});
+      return go(std::integral_constant<int, 256>{}, std::true_type{});
     }
     if (Cout <= 64) return go(std::integral_constant<int, 64>{}, std::false_type{});
-    return go(std::integral_constant<int, 128>{}, std::false_type{});
+    if (Cout < 256) return go(std::integral_constant<int, 128>{}, std::false_type{});
+    return go(std::integral_constant<int, 256>{}, std::false_type{});
   });
   return 0;
 }
@@ -626,17 +692,21 @@ int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
         if (M == 0) continue;
         RowMap rm{}; rm.mode = 2; rm.RH = g.RH; rm.RW = g.RW; rm.OH = H; rm.OW = W; rm.s = stride; rm.py = py; rm.px = px;
         auto go = [&](auto bn) -> int {
-          return with_cfg<T>(Cin <= 64 ? 3 : 1, [&](auto C) -> int {
-            constexpr int BM = decltype(C)::BM, NST = decltype(C)::NST;
-            constexpr int BN = decltype(bn)::value < decltype(C)::BN ? decltype(bn)::value : decltype(C)::BN;
-            ConvDgradA<T, BM, decltype(C)::W> la{}; la.dy = (const T*)dy; la.g = g; la.M = M;
-            ConvDgradB<T, BN, decltype(C)::W> lb{}; lb.w = (const T*)wp; lb.g = g; lb.NC = Cin;
+          return with_cfg<T>(Cin <= 64 ? 3 : 1, [&](auto C0) -> int {
+            typedef ConvCfg<decltype(C0), decltype(bn)::value> CC;
+            constexpr int BM = CC::BM, NST = CC::NST;
+            constexpr int BN = decltype(bn)::value < CC::BN ? decltype(bn)::value : CC::BN;
+            constexpr int LN = CC::PP ? CC::LN : BN;
+            CC C{};
+            ConvDgradA<T, CC::LM, CC::W> la{}; la.dy = (const T*)dy; la.g = g; la.M = M;
+            ConvDgradB<T, LN, CC::W> lb{}; lb.w = (const T*)wp; lb.g = g; lb.NC = Cin;
             EpiStd<T, T> e{(T*)dx, (long)Cin, 0, bias, scale, shift, (const T*)res1, (long)Cin, (const T*)res2, (long)Cin,
                            (T*)pre, (long)Cin, stats, act, M, N, rm, colsum};
             return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, M, N, cdiv(K, KT<T>::BK), 1, 1, st);
           });
         };
-        int rc = Cin <= 64 ? go(std::integral_constant<int, 64>{}) : go(std::integral_constant<int, 128>{});
+        int rc = Cin <= 64 ? go(std::integral_constant<int, 64>{})
+                           : (Cin < 256 ? go(std::integral_constant<int, 128>{}) : go(std::integral_constant<int, 256>{}));
         if (rc) return rc;
       }
   });
