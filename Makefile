@@ -9,6 +9,17 @@ FLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -munsafe-fp-atomics -mllvm 
 
 all: s3od_amd/libs3od_hip.so
 
+# attention: no SLP vectorisation -- hipcc packs the P*dP / P*V products into v_pk_mul_f32 on
+# register pairs that do not match the bf16 packing, then repairs them with v_mov / v_alignbit /
+# v_perm (dK/dV loop: 185 -> 145 VALU per 64 MFMA without it; attention backward 3144 -> 3019 us at
+# bs 16, N 4101, same box); packed f32 VALU beside MFMAs
+# is an anti-lever on CDNA4 anyway
+ATTN_FLAGS := -fno-slp-vectorize
+
+build/attention.o: $(CSRC)/attention.hip $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(FLAGS) $(ATTN_FLAGS) -c $< -o $@
+
 build/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(FLAGS) -c $< -o $@
