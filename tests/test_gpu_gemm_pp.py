@@ -1,0 +1,138 @@
+"""GPU parity of the 256x256 ping-pong GEMM kernel (gemm.hpp igemm_pp_kernel) through the C ABI.
+
+The production ViT linears (M = 16 * 4101 = 65616 token rows) run on it; the model-level tests
+reach it only at the full-size configurations, so this file pins the kernel itself at sizes that
+exercise its paths: the M-tail launch (rows past the last 256-row panel go to a second, 128x128
+launch), K tails (K % 64 != 0: zero-filled by the buffer range check), the epilogue variants the
+engine uses (bias, LayerScale, fp32 residual, pre-activation store, GELU, GELU' dgrad, in-place
+fp32 accumulate), QKV + RoPE with a token-row offset in the tail launch, and split-K wgrad.
+
+Reference: fp32 torch on the same bf16 operands.  Tolerances: rel-L2 <= 1e-5 for fp32 outputs
+(fp32 accumulation; only the summation order differs), <= 4e-3 for bf16 outputs (one bf16
+rounding, 2^-9 relative), GELU paths <= 5e-3 (the branch-free bf16-mode erf is 1.5e-7 absolute).
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+BF16, ACT_GELU, ACT_GELU_BWD = 1, 2, 3
+
+
+def _lib():
+    from s3od_amd._lib import lib, stream
+    return lib(), stream()
+
+
+def rel_l2(a, b):
+    a = a.double(); b = b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def r(*s, dt=torch.bfloat16, scale=1.0):
+    return (torch.randn(*s, device="cuda") * scale).to(dt)
+
+
+@pytest.mark.parametrize("M,N,K", [(16384 + 80, 768, 768), (16384 + 80, 2304, 776), (16384, 1280, 3072),
+                                   (17000, 768, 136)])
+def test_pp_linear_fwd_residual_pre(M, N, K):
+    """o_proj / down-projection form: out_f32 = (x w^T + b) * ls + res (fp32), pre (bf16) stored."""
+    torch.manual_seed(M + N + K)
+    L, s = _lib()
+    x, w = r(M, K), r(N, K, scale=K ** -0.5)
+    b, ls = r(N, dt=torch.float32), r(N, dt=torch.float32)
+    res = r(M, N, dt=torch.float32)
+    out = torch.empty(M, N, device="cuda")
+    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    L("s3od_linear_fwd", BF16, M, N, K, x, K, w, b, ls, None, 0, res, N, None, 0, 1, out, N, 1, pre, N, 0, 0, 0, s)
+    ref_pre = x.float() @ w.float().t() + b
+    ref = ref_pre * ls + res
+    torch.cuda.synchronize()
+    assert rel_l2(out, ref) < 1e-5
+    assert rel_l2(pre.float(), ref_pre) < 4e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(16384 + 80, 3072, 768), (16384 + 80, 1792, 200)])
+def test_pp_linear_fwd_gelu(M, N, K):
+    """up-projection form: out = GELU(x w^T + b) in bf16, pre stored."""
+    torch.manual_seed(M + N)
+    L, s = _lib()
+    x, w, b = r(M, K), r(N, K, scale=K ** -0.5), r(N, dt=torch.float32)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    L("s3od_linear_fwd", BF16, M, N, K, x, K, w, b, None, None, ACT_GELU, None, N, None, 0, 0, out, N, 0, pre, N, 0, 0, 0, s)
+    ref_pre = x.float() @ w.float().t() + b
+    ref = torch.nn.functional.gelu(ref_pre)
+    torch.cuda.synchronize()
+    assert rel_l2(pre.float(), ref_pre) < 4e-3
+    assert rel_l2(out.float(), ref) < 5e-3
+
+
+def test_pp_qkv_rope_tail():
+    """QKV + RoPE + head split at 4 images of 4101 tokens (M tail of 4 * 4101 % 256 = 20 rows):
+    the tail launch must address the global token rows."""
+    torch.manual_seed(3)
+    L, s = _lib()
+    B, Nt, P, H = 4, 4101, 4096, 12
+    D = 64 * H
+    x, w, b = r(B * Nt, D), r(3 * D, D, scale=D ** -0.5), r(3 * D, dt=torch.float32)
+    ang = torch.rand(P, 32, device="cuda") * 6.28
+    cs = torch.cat([ang.cos(), ang.cos()], 1).contiguous()
+    sn = torch.cat([ang.sin(), ang.sin()], 1).contiguous()
+    q, k, v = (torch.empty(B * H, Nt, 64, device="cuda", dtype=torch.bfloat16) for _ in range(3))
+    L("s3od_qkv_rope_fwd", BF16, B, Nt, P, H, x, w, b, cs, sn, q, k, v, s)
+    y = x.float() @ w.float().t() + b                              # [B*Nt, 3D]
+    y = y.view(B, Nt, 3, H, 64).permute(2, 0, 3, 1, 4).reshape(3, B * H, Nt, 64)
+    def rope(t):
+        t = t.clone()
+        pt = t[:, Nt - P:]
+        rot = torch.cat([-pt[..., 32:], pt[..., :32]], -1)
+        t[:, Nt - P:] = pt * cs + rot * sn
+        return t
+    QSCALE = 0.125 * 1.4426950408889634              # q pre-scaled by log2(e)/8 (common.hpp)
+    torch.cuda.synchronize()
+    assert rel_l2(q.float(), rope(y[0]) * QSCALE) < 4e-3
+    assert rel_l2(k.float(), rope(y[1])) < 4e-3
+    assert rel_l2(v.float(), y[2]) < 4e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(16384 + 80, 768, 3072), (16384 + 80, 768, 2304)])
+def test_pp_linear_dgrad_accumulate(M, N, K):
+    """up / qkv dgrad form: dx (fp32) += dy w, accumulated in place into the residual gradient."""
+    torch.manual_seed(K)
+    L, s = _lib()
+    dy, w = r(M, K), r(K, N, scale=K ** -0.5)
+    dx0 = r(M, N, dt=torch.float32)
+    dx = dx0.clone()
+    L("s3od_linear_dgrad", BF16, M, N, K, dy, K, w, 0, dx, N, dx, N, 1, 0, 0, 0, None, s)
+    ref = dx0 + dy.float() @ w.float()
+    torch.cuda.synchronize()
+    assert rel_l2(dx, ref) < 1e-5
+
+
+def test_pp_linear_dgrad_gelu_bwd():
+    """down-projection dgrad form (GELU' by the saved pre-activation), bf16 out."""
+    torch.manual_seed(7)
+    L, s = _lib()
+    M, N, K = 16384 + 80, 3072, 768
+    dy, w, pre = r(M, K), r(K, N, scale=K ** -0.5), r(M, N)
+    dx = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    L("s3od_linear_dgrad", BF16, M, N, K, dy, K, w, ACT_GELU_BWD, pre, N, dx, N, 0, 0, 0, 0, None, s)
+    p = pre.float().requires_grad_(True)
+    g = torch.autograd.grad(torch.nn.functional.gelu(p), p, dy.float() @ w.float())[0]
+    torch.cuda.synchronize()
+    assert rel_l2(dx.float(), g) < 5e-3
+
+
+@pytest.mark.parametrize("Nout,Kin,rows", [(3072, 768, 16384 + 80), (768, 3072, 16384 + 80), (2304, 768, 20000)])
+def test_pp_linear_wgrad_split(Nout, Kin, rows):
+    """split-K wgrad (fp32 atomics) accumulating onto an existing gradient."""
+    torch.manual_seed(rows)
+    L, s = _lib()
+    dy, x = r(rows, Nout), r(rows, Kin)
+    dw0 = r(Nout, Kin, dt=torch.float32)
+    dw = dw0.clone()
+    L("s3od_linear_wgrad", BF16, Nout, Kin, rows, dy, Nout, x, Kin, dw, 0, s)
+    ref = dw0 + dy.float().t() @ x.float()
+    torch.cuda.synchronize()
+    assert rel_l2(dw, ref) < 1e-5
