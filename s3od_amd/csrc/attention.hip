@@ -52,10 +52,20 @@ template <typename T> struct Stage {
   static constexpr int CH = 64 * 64 * sizeof(T) / 16 / 256;   // 16-B chunks per thread per tile
   uint4 k[CH], v[CH];
   DEV void load(const T* K, const T* V, int key0, int N, int tid) {
+    constexpr int CPR = 64 * sizeof(T) / 16;
+    if (key0 + 64 <= N) {             // whole tile in range (uniform): no per-key selects
+#pragma unroll
+      for (int i = 0; i < CH; i++) {
+        const int c = tid + 256 * i;
+        const long o = (long)(key0 + c / CPR) * 64 + (c % CPR) * (16 / sizeof(T));
+        k[i] = *(const uint4*)(K + o);
+        v[i] = *(const uint4*)(V + o);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < CH; i++) {
       int c = tid + 256 * i;
-      constexpr int CPR = 64 * sizeof(T) / 16;
       int key = key0 + c / CPR, col = (c % CPR) * (16 / sizeof(T));
       bool ok = key < N;
       k[i] = ok ? *(const uint4*)(K + (long)key * 64 + col) : make_uint4(0, 0, 0, 0);
