@@ -22,7 +22,9 @@ class _DPTFn(torch.autograd.Function):
         out = eng.forward(x, train=True, rope_rescale=rescale, ctx=ctx)
         fctx.s3od = (model, eng, ctx)
         fctx.set_materialize_grads(False)     # an output the loss never reads arrives as None, not zeros
-        fctx.mark_non_differentiable(out["features"])
+        # features (= path_1, NCHW view of the NHWC decoder tensor) carries grad like the reference's:
+        # its gradient joins path_1's in the native backward.  The input images get no gradient
+        # (data, never a leaf that requires grad in the reference's training).
         return out["pred_masks"], out["pred_iou"], out["features"]
 
     @staticmethod
@@ -37,7 +39,7 @@ class _DPTFn(torch.autograd.Function):
             d_iou = torch.zeros((ctx.B, nm), dtype=torch.float32, device=G["_flat"].device)
         eng.grad_hook = model._grad_ready_hook
         try:
-            eng.backward(ctx, d_masks.float().contiguous(), d_iou.float().contiguous(), G)
+            eng.backward(ctx, d_masks.float().contiguous(), d_iou.float().contiguous(), G, d_feat=d_feat)
         finally:
             eng.grad_hook = None
             fctx.s3od = None

@@ -471,7 +471,7 @@ class DPTEngine:
         dx1 = self._rcu_bwd(ds, r, 1, B, ctx, G)
         return ds, dx1
 
-    def decoder_backward(self, ctx, d_logits, d_iou, G):
+    def decoder_backward(self, ctx, d_logits, d_iou, G, d_feat=None):
         lib().phase = "decoder"
         L, P, W8, dt = lib(), self.p, self.w, self.dt
         st = stream()
@@ -503,6 +503,8 @@ class DPTEngine:
         # ---- output_conv1 3x3 256->128
         self._wgrad_conv(doc1, p1, B, H1, W1, 256, H1, W1, 128, 3, 1, 1, G[m + "output_conv1.weight"])
         dp1 = self._dgrad_conv(doc1, W8["oc1"], B, H1, W1, 256, H1, W1, 128, 3, 1, 1)
+        if d_feat is not None:     # gradient of the returned features (= path_1, NCHW view)
+            dp1.add_(d_feat.permute(0, 2, 3, 1).to(dp1.dtype))
         # ---- classifier head -> broadcast gradient onto path_1 (folded into the bilinear backward)
         dpix = torch.empty((B, 256), dtype=torch.float32, device=dev)
         L("s3od_iou_head_bwd", hd["pooled"], hd["hid"], P[h + "classifier_head.2.weight"], P[h + "classifier_head.4.weight"],
@@ -613,10 +615,11 @@ class DPTEngine:
 
     grad_hook = None
 
-    def backward(self, ctx: Ctx, d_logits, d_iou, G):
+    def backward(self, ctx: Ctx, d_logits, d_iou, G, d_feat=None):
         """Accumulate parameter gradients into G (name -> fp32 tensor, reference layout; plus the
-        fused views 'qkv_w{i}', 'heads1_w', 'heads1_b', 'heads2_w', 'heads2_b')."""
-        dtaps = self.decoder_backward(ctx, d_logits, d_iou, G)
+        fused views 'qkv_w{i}', 'heads1_w', 'heads1_b', 'heads2_w', 'heads2_b').  d_feat: optional
+        gradient of the returned ``features`` (NCHW), added to path_1's."""
+        dtaps = self.decoder_backward(ctx, d_logits, d_iou, G, d_feat=d_feat)
         if self.grad_hook is not None:
             self.grad_hook("seg_head")
         self.encoder_backward(ctx, dtaps, G)

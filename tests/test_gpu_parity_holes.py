@@ -9,7 +9,8 @@
 * the antialiased post-resize (predictor.py:117-123) vs F.interpolate(antialias=True) at 480x640,
   2000x2000 and 800x400;
 * a transformers-4.x (``encoder.layer.N``) checkpoint loads through BackgroundRemoval;
-* reference Quirk 2 (predictor.py:83-90: pad 0 but new_w < S feeds the S x new_w image).
+* reference Quirk 2 (predictor.py:83-90: pad 0 but new_w < S feeds the S x new_w image);
+* the gradient of the returned ``features`` (path_1) joins the native backward (vs the oracle).
 """
 import numpy as np
 import pytest
@@ -187,3 +188,45 @@ def test_quirk2_unpadded_input():
     br.exact_reference_quirks = False
     x2, _ = br._preprocess(img)
     assert tuple(x2.shape) == (1, 3, 1024, 1024)
+
+
+def test_features_gradient_vs_oracle():
+    """``features`` (path_1) carries grad as in the reference: loss = mask loss + <features, R> on the
+    f32-strict HIP path vs the oracle's autograd (per-parameter grad norm <= 2e-3, cosine >= 0.999)."""
+    from oracle import s3od_oracle as O
+    from s3od_amd.loss import LossModule, FOCAL_IOU
+    from s3od_amd.model import DPTSegmentation
+    from s3od_amd.weights import synthetic_state_dict
+    from bench import synthetic_batch
+    torch.manual_seed(5)
+    x, masks = synthetic_batch(1, 224, 41, torch.device("cuda"))
+    m = DPTSegmentation(compute_dtype="f32").cuda().train()
+    m._rope_rescale = 1.0
+    m.zero_grad(set_to_none=True)
+    out = m(x)
+    R = torch.randn_like(out["features"]) * 1e-3
+    lm = LossModule(FOCAL_IOU, full_mask_lambda=0.1, decay_rate=0.2)
+    loss, _ = lm(out, {"images": x, "masks": masks}, 0)
+    (loss + (out["features"] * R).sum()).backward()
+    torch.cuda.synchronize()
+    sd = {}
+    for k, v in synthetic_state_dict(0).items():
+        t = torch.from_numpy(v).cuda()
+        if t.is_floating_point() and "running" not in k:
+            t.requires_grad_(True)
+        sd[k] = t
+    ref = O.forward(x, sd, train=True, rope_rescale=1.0)
+    rloss, *_ = O.multi_mask_loss(ref, masks, 0)
+    (rloss + (ref["features"] * R).sum()).backward()
+    worst_n, worst_c = (0.0, ""), (1.0, "")
+    for n, p in m.named_parameters():
+        if p.grad is None:
+            continue
+        if "resConfUnit" in n and (n.endswith("conv1.bias") or n.endswith("conv2.bias")):
+            continue     # a bias feeding train-mode BN has an exactly-zero true gradient (noise only)
+        g, rg = p.grad.double(), sd[n].grad.double()
+        en = abs(float(g.norm()) - float(rg.norm())) / max(float(rg.norm()), 1e-12)
+        c = float((g.reshape(-1) @ rg.reshape(-1)) / (g.norm() * rg.norm()).clamp_min(1e-30))
+        worst_n = max(worst_n, (en, n)); worst_c = min(worst_c, (c, n))
+    assert worst_n[0] <= 2e-3, worst_n
+    assert worst_c[0] >= 0.999, worst_c
