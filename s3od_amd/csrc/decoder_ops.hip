@@ -283,6 +283,44 @@ __global__ void bilinear_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, 
   store8<T>(y + i, o);
 }
 
+// exact 2x upsampling: one thread = 8 channels of the 2x2 output block (2k..2k+1, 2j..2j+1), read
+// from the clamped 3x3 input neighbourhood of (k, j) (9 loads for 4 outputs instead of 16).  Output
+// row 2k takes neighbourhood rows (0, 1) and 2k+1 rows (1, 2) with bil_coef's weights; at the borders
+// bil_coef's clamped taps coincide with the clamped neighbourhood rows (or carry weight 0), so every
+// output is computed by the same expression as bilinear_fwd_kernel.
+template <typename T>
+__global__ void bilinear_up2_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int IH, int IW, int C) {
+  long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  long total = (long)B * IH * IW * C;
+  if (i >= total) return;
+  const int c = i % C; long pix = i / C;
+  const int j = pix % IW; long r = pix / IW; const int k = r % IH; const int b = r / IH;
+  const int OH = 2 * IH, OW = 2 * IW;
+  const int ry[3] = {max(k - 1, 0), k, min(k + 1, IH - 1)}, rx[3] = {max(j - 1, 0), j, min(j + 1, IW - 1)};
+  const T* base = x + (long)b * IH * IW * C + c;
+  float n[3][3][8];
+#pragma unroll
+  for (int a = 0; a < 3; a++)
+#pragma unroll
+    for (int e = 0; e < 3; e++) load8<T>(base + ((long)ry[a] * IW + rx[e]) * C, n[a][e]);
+#pragma unroll
+  for (int dy = 0; dy < 2; dy++) {
+    int y0, y1; float wy0, wy1;
+    bil_coef(2 * k + dy, IH, OH, y0, y1, wy0, wy1);
+#pragma unroll
+    for (int dx = 0; dx < 2; dx++) {
+      int x0, x1; float wx0, wx1;
+      bil_coef(2 * j + dx, IW, OW, x0, x1, wx0, wx1);
+      const float* a = n[dy][dx]; const float* bb = n[dy][dx + 1];
+      const float* cc = n[dy + 1][dx]; const float* d = n[dy + 1][dx + 1];
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; e++) o[e] = wy0 * (wx0 * a[e] + wx1 * bb[e]) + wy1 * (wx0 * cc[e] + wx1 * d[e]);
+      store8<T>(y + (((long)b * OH + 2 * k + dy) * OW + 2 * j + dx) * C + c, o);
+    }
+  }
+}
+
 // gather-form backward: dx[i] = sum over outputs whose (i0 or i1) == i of weight * (dy + bcast[b,c])
 template <typename T>
 __global__ void bilinear_bwd_kernel(const T* __restrict__ dy, const float* __restrict__ bcast, T* __restrict__ dx,
@@ -550,7 +588,12 @@ int s3od_bilinear_fwd(int dtype, const void* x, void* y, int B, int IH, int IW, 
   S3OD_REQUIRE(C % 8 == 0, "bilinear: C %% 8");
   long total = (long)B * OH * OW * C / 8;
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(bilinear_fwd_kernel<T>, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, B, IH, IW, OH, OW, C);
+    if (OH == 2 * IH && OW == 2 * IW) {
+      const long t2 = (long)B * IH * IW * C / 8;
+      hipLaunchKernelGGL(bilinear_up2_kernel<T>, dim3(cdiv(t2, 256)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, B, IH, IW, C);
+    } else {
+      hipLaunchKernelGGL(bilinear_fwd_kernel<T>, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream, (const T*)x, (T*)y, B, IH, IW, OH, OW, C);
+    }
   });
   return s3od_check_launch("bilinear_fwd");
 }
