@@ -236,7 +236,7 @@ conv3x3_halo_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EPI 
       const int c = tid + 512 * i;
       if (c < S::HCH) { const int px = c / CPP, ch = c - px * CPP; *(uint4*)(halo + swz16(px, ch)) = hr[i]; }
     }
-    __syncthreads();
+    lds_barrier();                                    // LDS only: a __syncthreads() would drain the stores
     if (tile + wpx < t_end) prefetch(tile + wpx);     // next tile's halo in flight during the MFMAs
     f32x4 acc[2][NB];
 #pragma unroll
@@ -261,7 +261,7 @@ conv3x3_halo_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EPI 
           for (int nb = 0; nb < NB; nb++) acc[pb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nb], fa[pb], acc[pb][nb], 0, 0, 0);
       }
     }
-    __syncthreads();                                  // halo consumed: its region now stages C
+    lds_barrier();                                    // halo consumed: its region now stages C
     // lane owns C[px = pb*16 + lr][n = nb*16 + 4*lg .. +3] of output row `wave`
     float* ct = (float*)halo;
     const int vbase = tile * (HT_TH * HT_TW);
@@ -277,9 +277,9 @@ conv3x3_halo_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EPI 
             *(float4*)(ct + (rr + pb * 16 + lr) * S::LDT + nb * 16 + 4 * lg) =
                 make_float4(acc[pb][nb][0], acc[pb][nb][1], acc[pb][nb][2], acc[pb][nb][3]);
       }
-      __syncthreads();
+      lds_barrier();
       epi(ct, S::LDT, vbase + c0 * HT_TW, 0, tid, S::CR, COUT, 512);
-      __syncthreads();
+      lds_barrier();
     }
   }
 }
