@@ -510,7 +510,8 @@ int s3od_linear_fwd(int dtype, int M, int N, int K, const void* x, long ldx, con
       // measured (tools/lin_sweep.py, bs 16 1024^2): the 256x256 ping-pong kernel for the large ViT
       // linears (o_proj 241 -> 215 us, up 576 -> 563, down 487 -> 418); else 256x128 x 3 stages for
       // K >= 2048, 128x128 otherwise
-      const int def = (M >= 16384 && N >= 768 && N % 256 == 0) ? 5
+      // (plain bias-only epilogues stay on 128x128: the DPT projections M=65536 N=1024 K=768 157 -> 146 us)
+      const int def = (M >= 16384 && N >= 768 && N % 256 == 0 && (res1 || act == ACT_GELU || K >= 2048)) ? 5
                       : (K >= 2048 ? 0 : 1);
       return with_cfg<T>(def, [&](auto C) -> int {
         constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
