@@ -47,6 +47,13 @@ static bool split_tail(int M) {
   static const int knob = dev_knob("S3OD_M_TAIL", 1);
   return knob && tl_cfg < 0 && M > 256 && (M & 255) != 0;
 }
+// the 256x256 ping-pong kernel (one workgroup per CU) only pays when its tiles fill whole rounds of
+// the 256 CUs: at bs 8 (M = 32808) o_proj / down-projection / QKV have 384 / 384 / 1152 tiles = 1.5 /
+// 1.5 / 4.5 rounds, where the 128x128 config (2 per CU) runs whole rounds (o_proj 138 us at 281 TF/s)
+static bool pp_pays(int M, int N) {
+  const long tiles = (long)(M / 256) * cdiv(N, 256), rounds = (tiles + 255) / 256;
+  return tiles >= 256 && (double)tiles / (double)(rounds * 256) >= 0.95;
+}
 template <typename T, class F> static int with_cfg(int def, F f) {
   int c = tl_cfg >= 0 ? tl_cfg : gemm_cfg(); if (c < 0) c = def;
   switch (c) {
@@ -511,7 +518,7 @@ int s3od_linear_fwd(int dtype, int M, int N, int K, const void* x, long ldx, con
       // linears (o_proj 241 -> 215 us, up 576 -> 563, down 487 -> 418); else 256x128 x 3 stages for
       // K >= 2048, 128x128 otherwise
       // (plain bias-only epilogues stay on 128x128: the DPT projections M=65536 N=1024 K=768 157 -> 146 us)
-      const int def = (M >= 16384 && N >= 768 && N % 256 == 0 && (res1 || act == ACT_GELU || K >= 2048)) ? 5
+      const int def = (pp_pays(M, N) && N % 256 == 0 && (res1 || act == ACT_GELU || K >= 2048)) ? 5
                       : (K >= 2048 ? 0 : 1);
       return with_cfg<T>(def, [&](auto C) -> int {
         constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
@@ -554,7 +561,7 @@ int s3od_linear_dgrad(int dtype, int M, int N, int K, const void* dy, long lddy,
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(K, KT<T>::BK);
     // ping-pong 256x256 for the long-K dgrads (up 441 -> 374 us, qkv 334 -> 292); 128x128 for K = 768
-    const int def = (M >= 16384 && K >= 2048 && N % 256 == 0) ? 5 : 1;
+    const int def = (pp_pays(M, N) && K >= 2048 && N % 256 == 0) ? 5 : 1;
     return with_cfg<T>(def, [&](auto C) -> int {
       constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
       DenseKC<T, decltype(C)::LM, decltype(C)::W> la{(const T*)dy, lddy, M, K, 0};
@@ -600,7 +607,7 @@ int s3od_qkv_rope_fwd(int dtype, int B, int Ntok, int P, int H, const void* x, c
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     auto part = [&](int m_first, int M) -> int {
-      return with_cfg<T>(5, [&](auto C) -> int {
+      return with_cfg<T>(pp_pays(M, N) ? 5 : 1, [&](auto C) -> int {
         constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
         DenseKC<T, decltype(C)::LM, decltype(C)::W> la{(const T*)x + (long)m_first * D, (long)D, M, D, 0};
         DenseKC<T, decltype(C)::LN, decltype(C)::W> lb{(const T*)w, (long)D, N, D, 0};
