@@ -816,6 +816,23 @@ template <class F> DEV void for_segments(const float* ct, int LDT, int BM, int B
   }
 }
 
+// 8 consecutive elements held raw (16 B for bf16, 32 B for f32) until they are consumed
+template <typename T> struct Row8;
+template <> struct Row8<float> {
+  float4 a, b;
+  DEV void load(const float* p) { a = ((const float4*)p)[0]; b = ((const float4*)p)[1]; }
+  DEV void get(float* v) const { v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w; }
+};
+template <> struct Row8<bf16> {
+  uint4 u;
+  DEV void load(const bf16* p) { u = *(const uint4*)p; }
+  DEV void get(float* v) const {
+    const bf16x8 x = __builtin_bit_cast(bf16x8, u);
+#pragma unroll
+    for (int e = 0; e < 8; e++) v[e] = (float)x[e];
+  }
+};
+
 // ------------------------------------------------------------------ common epilogue
 // out = act(acc*scale[n] + shift[n]) + res1 + res2 ; optional raw store (pre-act) and BN
 // batch statistics (sum / sum of squares of the pre-activation value, fp64 atomics).
@@ -850,7 +867,27 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
       }
     }
     const bool fixed_cols = NT % (BN / 8) == 0;
-    for_segments(ct, LDT, BM, BN, m0, n0, M, N, tid, NT, [&](int m, int n, const float* a, int, int) {
+    // residual rows of a thread with <= 4 segments are all loaded before its first store: inside the
+    // segment loop each load would come after the previous segment's stores, and its wait (vmcnt is
+    // in issue order) would drain them.  Rows outside the output load row 0 (address select, not a
+    // branch around the load).  Larger tiles (the ping-pong kernel's 8 segments) keep the loop form:
+    // 8 prefetched rows beside its live accumulators spill.  bf16 residuals only (the GELU'/ReLU'
+    // pre-activations of dgrad, 587 vs 617 us for down-dgrad N3072 K768); the f32 residual-stream
+    // adds of o_proj/down fwd measured 1-2% slower with their 32 B rows held.
+    constexpr int PF = 4;
+    const int spr_ = BN / 8, rpi_ = NT / spr_;
+    const bool pf = sizeof(TR) == 2 && (res1 != nullptr) && fixed_cols && BM % rpi_ == 0 && BM / rpi_ <= PF;
+    Row8<TR> pr1[PF];
+    if (pf) {
+      const int r0 = tid / spr_, nn = n0 + (tid % spr_) * 8;
+#pragma unroll
+      for (int it = 0; it < PF; it++) {
+        const int m = m0 + r0 + it * rpi_;
+        const long o = (it < BM / rpi_ && m < M && nn < N) ? rm.map(m) : -1;
+        pr1[it].load(res1 + (o >= 0 ? o : 0) * ldr1 + (nn < N ? nn : 0));
+      }
+    }
+    for_segments(ct, LDT, BM, BN, m0, n0, M, N, tid, NT, [&](int m, int n, const float* a, int r, int) {
       float pv[8], v[8], o[8];
       const long orow = rm.map(m);
       if (orow < 0) return;                 // spatial-tile row outside the image (RowMap mode 3)
@@ -864,12 +901,19 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
       if (pre) store8<TP>(pre + orow * ldp + n, pv);
       // act is uniform: branch once per segment, so the erf path is never speculated for the others
       constexpr bool FAST = sizeof(TP) == 2;     // bf16 compute: branch-free GELU (common.hpp)
+      float rp[8];
+      if (pf) {
+        const int it = (r - tid / spr_) / rpi_;            // compile-time after for_segments unrolls
+#pragma unroll
+        for (int q = 0; q < PF; q++)
+          if (q == it) pr1[q].get(rp);
+      }
       if (act == ACT_GELU_BWD) {
-        float r[8]; load8<TR>(res1 + orow * ldr1 + n, r);
+        float r[8]; if (pf) { for (int e = 0; e < 8; e++) r[e] = rp[e]; } else load8<TR>(res1 + orow * ldr1 + n, r);
 #pragma unroll
         for (int e = 0; e < 8; e++) o[e] = v[e] * (FAST ? gelu_fast_grad(r[e]) : gelu_erf_grad(r[e]));
       } else if (act == ACT_RELU_BWD) {
-        float r[8]; load8<TR>(res1 + orow * ldr1 + n, r);
+        float r[8]; if (pf) { for (int e = 0; e < 8; e++) r[e] = rp[e]; } else load8<TR>(res1 + orow * ldr1 + n, r);
 #pragma unroll
         for (int e = 0; e < 8; e++) o[e] = r[e] > 0.f ? v[e] : 0.f;
       } else {
@@ -883,7 +927,7 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
 #pragma unroll
           for (int e = 0; e < 8; e++) o[e] = v[e];
         }
-        if (res1) { float r[8]; load8<TR>(res1 + orow * ldr1 + n, r);
+        if (res1) { float r[8]; if (pf) { for (int e = 0; e < 8; e++) r[e] = rp[e]; } else load8<TR>(res1 + orow * ldr1 + n, r);
 #pragma unroll
           for (int e = 0; e < 8; e++) o[e] += r[e]; }
       }
