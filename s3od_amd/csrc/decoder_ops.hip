@@ -96,7 +96,7 @@ __global__ void affine_act_kernel(const T* __restrict__ x, const float* __restri
   float v[8], s[8], t[8];
   load8<T>(x + i, v); load8<float>(scale + c, s); load8<float>(shift + c, t);
 #pragma unroll
-  for (int e = 0; e < 8; e++) { v[e] = v[e] * s[e] + t[e]; if (act == 1) v[e] = fmaxf(v[e], 0.f); }
+  for (int e = 0; e < 8; e++) { v[e] = __builtin_fmaf(v[e], s[e], t[e]); if (act == 1) v[e] = fmaxf(v[e], 0.f); }
   if (r1) { float r[8]; load8<T>(r1 + i, r);
 #pragma unroll
     for (int e = 0; e < 8; e++) v[e] += r[e]; }
@@ -124,10 +124,28 @@ template <int NV> DEV void rowphase_reduce(float (&v)[NV][8], float* red, int t,
   }
 }
 
-// BN backward, pass 1: per channel sums of dy' and dy'*xhat where dy' = dy (or dy*(y>0) if RELU)
+// ReLU masks of the BN backward.  MODE 0: none; 1: dy' = dy*(y>0) with y read back; 2: y recomputed
+// as T(fma(z, scale, shift)) — the exact value affine_act_kernel stored — so the y tensor is not read
+// (two of the seven tensor passes of the two-pass backward).
+template <typename T, int MODE> struct ReluMask {
+  const T* y; float s[8], t[8];
+  DEV void init(const T* y_, const float* as, const float* at, int c) {
+    y = y_;
+    if (MODE == 2) { load8<float>(as + c, s); load8<float>(at + c, t); }
+  }
+  DEV void load(long o, float* yy) const { if (MODE == 1) load8<T>(y + o, yy); }
+  DEV bool on(const float* zz, const float* yy, int e) const {
+    if (MODE == 0) return true;
+    if (MODE == 1) return yy[e] > 0.f;
+    return (float)(T)__builtin_fmaf(zz[e], s[e], t[e]) > 0.f;
+  }
+};
+
+// BN backward, pass 1: per channel sums of dy' and dy'*xhat where dy' = dy masked by ReluMask,
 // xhat = (z - mean)*rstd.  Output double [2][C].  Main loop keeps 4 pixel rows of loads in flight.
-template <typename T, bool RELU>
+template <typename T, int MODE>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ z, const T* __restrict__ y_relu,
+                                     const float* __restrict__ as, const float* __restrict__ at,
                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                      double* __restrict__ sums, long npix, int C, int pix_per_block) {
   __shared__ float red[256 * 8];
@@ -136,12 +154,13 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict_
   const int c = cgi * 8;
   float mu[8], rs[8];
   load8<float>(mean + c, mu); load8<float>(rstd + c, rs);
+  ReluMask<T, MODE> rl; rl.init(y_relu, as, at, c);
   float acc[2][8] = {{0, 0, 0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0, 0}};
   const long p0 = (long)blockIdx.x * pix_per_block, p1 = min(npix, p0 + pix_per_block);
   auto body = [&](const float* d0, const float* zz, const float* yy) {
 #pragma unroll
     for (int e = 0; e < 8; e++) {
-      float d = (RELU && !(yy[e] > 0.f)) ? 0.f : d0[e];
+      float d = rl.on(zz, yy, e) ? d0[e] : 0.f;
       float xh = (zz[e] - mu[e]) * rs[e];
       acc[0][e] += d; acc[1][e] += d * xh;
     }
@@ -153,7 +172,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict_
     for (int j = 0; j < 4; j++) {
       const long o = (p + j * rows) * C + c;
       load8<T>(dy + o, d[j]); load8<T>(z + o, zz[j]);
-      if (RELU) load8<T>(y_relu + o, yy[j]);
+      rl.load(o, yy[j]);
     }
 #pragma unroll
     for (int j = 0; j < 4; j++) body(d[j], zz[j], yy[j]);
@@ -162,7 +181,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict_
     float d[8], zz[8], yy[8];
     const long o = p * C + c;
     load8<T>(dy + o, d); load8<T>(z + o, zz);
-    if (RELU) load8<T>(y_relu + o, yy);
+    rl.load(o, yy);
     body(d, zz, yy);
   }
   rowphase_reduce<2>(acc, red, t, cg);
@@ -184,8 +203,9 @@ __global__ void bn_fold_replicas_kernel(double* sums, int C) {
 
 // BN backward, pass 2: dz = w*rstd*(dy' - s1/n - xhat*s2/n); optional dcb[c] += sum_p dz (the
 // bias gradient of the conv that produced z).
-template <typename T, bool RELU>
+template <typename T, int MODE>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ z, const T* __restrict__ y_relu,
+                                    const float* __restrict__ as, const float* __restrict__ at,
                                     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ w,
                                     double* __restrict__ sums, T* __restrict__ dz, float* __restrict__ dcb,
                                     long npix, int C, int pix_per_block) {
@@ -199,13 +219,14 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
     mu[e] = mean[c + e]; rs[e] = rstd[c + e]; k1[e] = w[c + e] * rs[e];
     m1[e] = (float)(sums[c + e] / (double)npix); m2[e] = (float)(sums[C + c + e] / (double)npix);
   }
+  ReluMask<T, MODE> rl; rl.init(y_relu, as, at, c);
   float acc[1][8] = {{0, 0, 0, 0, 0, 0, 0, 0}};
   const long p0 = (long)blockIdx.x * pix_per_block, p1 = min(npix, p0 + pix_per_block);
   auto body = [&](long o, const float* d0, const float* zz, const float* yy) {
     float out[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) {
-      float d = (RELU && !(yy[e] > 0.f)) ? 0.f : d0[e];
+      float d = rl.on(zz, yy, e) ? d0[e] : 0.f;
       float xh = (zz[e] - mu[e]) * rs[e];
       out[e] = k1[e] * (d - m1[e] - xh * m2[e]);
       acc[0][e] += out[e];
@@ -219,7 +240,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
     for (int j = 0; j < 4; j++) {
       const long o = (p + j * rows) * C + c;
       load8<T>(dy + o, d[j]); load8<T>(z + o, zz[j]);
-      if (RELU) load8<T>(y_relu + o, yy[j]);
+      rl.load(o, yy[j]);
     }
 #pragma unroll
     for (int j = 0; j < 4; j++) body((p + j * rows) * C + c, d[j], zz[j], yy[j]);
@@ -228,7 +249,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
     float d[8], zz[8], yy[8];
     const long o = p * C + c;
     load8<T>(dy + o, d); load8<T>(z + o, zz);
-    if (RELU) load8<T>(y_relu + o, yy);
+    rl.load(o, yy);
     body(o, d, zz, yy);
   }
   if (dcb) {
@@ -559,8 +580,9 @@ int s3od_affine_act(int dtype, const void* x, const float* scale, const float* s
 }
 
 // sums: workspace of S3OD_NREP * 3 * C doubles (replicated [s1 | s2 | conv-bias] accumulators)
-int s3od_bn_bwd(int dtype, const void* dy, const void* z, const void* y_relu, const float* mean, const float* rstd,
-                const float* w, double* sums, void* dz, float* dw, float* db, float* dcb, long npix, int C, void* stream) {
+static int bn_bwd_impl(int dtype, const void* dy, const void* z, const void* y_relu, const float* as, const float* at,
+                       const float* mean, const float* rstd, const float* w, double* sums, void* dz, float* dw, float* db,
+                       float* dcb, long npix, int C, void* stream) {
   S3OD_REQUIRE(C % 8 == 0 && 256 % (C / 8) == 0, "bn_bwd: C");
   hipStream_t st = (hipStream_t)stream;
   (void)hipMemsetAsync(sums, 0, sizeof(double) * S3OD_NREP * 3 * C, st);
@@ -570,18 +592,32 @@ int s3od_bn_bwd(int dtype, const void* dy, const void* z, const void* y_relu, co
   ppb = (ppb + rows - 1) / rows * rows;
   const int nb = cdiv(npix, ppb);
   DISPATCH_T(dtype, {
-    auto go = [&](auto relu) {
-      constexpr bool R = decltype(relu)::value;
+    auto go = [&](auto mode) {
+      constexpr int R = decltype(mode)::value;
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, R>), dim3(nb), dim3(256), 0, st, (const T*)dy, (const T*)z, (const T*)y_relu,
-                         mean, rstd, sums, npix, C, (int)ppb);
+                         as, at, mean, rstd, sums, npix, C, (int)ppb);
       hipLaunchKernelGGL(bn_fold_replicas_kernel, dim3(cdiv(2 * C, 256)), dim3(256), 0, st, sums, C);
       hipLaunchKernelGGL((bn_bwd_apply_kernel<T, R>), dim3(nb), dim3(256), 0, st, (const T*)dy, (const T*)z,
-                         (const T*)y_relu, mean, rstd, w, sums, (T*)dz, dcb, npix, C, (int)ppb);
+                         (const T*)y_relu, as, at, mean, rstd, w, sums, (T*)dz, dcb, npix, C, (int)ppb);
     };
-    if (y_relu) go(std::true_type{}); else go(std::false_type{});
+    if (as) go(std::integral_constant<int, 2>{});
+    else if (y_relu) go(std::integral_constant<int, 1>{});
+    else go(std::integral_constant<int, 0>{});
   });
   hipLaunchKernelGGL(bn_param_grads_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, sums, dw, db, dcb, C);
   return s3od_check_launch("bn_bwd");
+}
+
+int s3od_bn_bwd(int dtype, const void* dy, const void* z, const void* y_relu, const float* mean, const float* rstd,
+                const float* w, double* sums, void* dz, float* dw, float* db, float* dcb, long npix, int C, void* stream) {
+  return bn_bwd_impl(dtype, dy, z, y_relu, nullptr, nullptr, mean, rstd, w, sums, dz, dw, db, dcb, npix, C, stream);
+}
+
+int s3od_bn_relu_bwd(int dtype, const void* dy, const void* z, const float* scale, const float* shift, const float* mean,
+                     const float* rstd, const float* w, double* sums, void* dz, float* dw, float* db, float* dcb, long npix,
+                     int C, void* stream) {
+  S3OD_REQUIRE(scale && shift, "bn_relu_bwd: scale/shift");
+  return bn_bwd_impl(dtype, dy, z, nullptr, scale, shift, mean, rstd, w, sums, dz, dw, db, dcb, npix, C, stream);
 }
 
 int s3od_bilinear_fwd(int dtype, const void* x, void* y, int B, int IH, int IW, int OH, int OW, int C, void* stream) {

@@ -446,7 +446,9 @@ class DPTEngine:
         self._wgrad_conv(dz2, c["a1"], B, h, w, 256, h, w, 256, 3, 1, 1, G[q + "conv2.weight"])
         da1 = self._dgrad_conv(dz2, W8[tag + ".c2"], B, h, w, 256, h, w, 256, 3, 1, 1)
         dz1 = torch.empty_like(d_out)
-        L("s3od_bn_bwd", self.dt, da1, c["z1"], c["a1"], c["bn1"]["mean"], c["bn1"]["rstd"], P[q + "bn1.weight"], sums, dz1,
+        # ReLU mask recomputed from z1 and bn1's scale/shift (bit-identical to a1 > 0): a1 is not read
+        L("s3od_bn_relu_bwd", self.dt, da1, c["z1"], c["bn1"]["scale"], c["bn1"]["shift"], c["bn1"]["mean"],
+          c["bn1"]["rstd"], P[q + "bn1.weight"], sums, dz1,
           G[q + "bn1.weight"], G[q + "bn1.bias"], G[q + "conv1.bias"], npix, 256, st)
         self._wgrad_conv(dz1, c["x"], B, h, w, 256, h, w, 256, 3, 1, 1, G[q + "conv1.weight"], relu_x=True)
         return self._dgrad_conv_res(dz1, W8[tag + ".c1"], B, h, w, 256, ACT_RELU_BWD, c["x"], d_out)

@@ -71,6 +71,9 @@ def cost(name, a):
     if n == "bn_bwd":
         dt, yrelu, npix, C = a[0], a[3], a[12], a[13]
         return "hbm", npix * C * _t(dt) * (3 + (yrelu is not None))
+    if n == "bn_relu_bwd":   # dy, z read, dz written (the ReLU mask is recomputed from z)
+        dt, npix, C = a[0], a[13], a[14]
+        return "hbm", npix * C * _t(dt) * 3
     if n == "avgpool":
         dt, B, HW, C = a[0], a[3], a[4], a[5]
         return "hbm", B * HW * C * _t(dt)

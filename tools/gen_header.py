@@ -35,6 +35,7 @@ REF = {
     "s3od_bn_finalize": "nn.BatchNorm2d train-mode batch statistics + running-stat update (momentum 0.1)",
     "s3od_affine_act": "BatchNorm apply + ReLU + residual: src/s3od/model.py:334-345, 383-393",
     "s3od_bn_bwd": "BatchNorm2d train-mode backward (reference: implicit torch autograd)",
+    "s3od_bn_relu_bwd": "BatchNorm2d + ReLU train-mode backward with the ReLU mask recomputed from z (reference: implicit torch autograd of src/s3od/model.py:334-345)",
     "s3od_bilinear_fwd": "F.interpolate(bilinear, align_corners=False): src/s3od/model.py:395-403",
     "s3od_bilinear_bwd": "F.interpolate backward (reference: implicit torch autograd)",
     "s3od_avgpool": "classifier_head AdaptiveAvgPool2d(1): src/s3od/model.py:185-191",
