@@ -378,7 +378,7 @@ int s3od_layernorm_fwd(int dtype, const float* x, const float* w, const float* b
 // ws: workspace of S3OD_NREP * 2 * D floats (replicated dw / db partials)
 int s3od_layernorm_bwd(int dtype, const void* dy, const float* x, const float* mean, const float* rstd, const float* w,
                        const float* dres, float* dx, float* dw, float* db, float* ws, int M, int D_, void* stream) {
-  const int rpb = 64;
+  static const int rpb = dev_knob("S3OD_LN_RPB", 32);
   hipStream_t st = (hipStream_t)stream;
   (void)hipMemsetAsync(ws, 0, sizeof(float) * S3OD_NREP * 2 * D_, st);
   DISPATCH_D(D_, {
@@ -413,7 +413,7 @@ int s3od_colsum(int dtype, const void* a, long lda, int M, int N, float* out, vo
 // ws: workspace of S3OD_NREP * 2 * D floats (replicated dlam / dbias partials)
 int s3od_layerscale_bwd(int dtype, const float* dx, const void* u, const float* lam, void* du, float* dlam, float* dbias,
                         float* ws, int M, int D_, void* stream) {
-  const int rpb = 64;
+  static const int rpb = dev_knob("S3OD_LS_RPB", 16);
   hipStream_t st = (hipStream_t)stream;
   (void)hipMemsetAsync(ws, 0, sizeof(float) * S3OD_NREP * 2 * D_, st);
   DISPATCH_D(D_, {

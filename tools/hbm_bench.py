@@ -37,6 +37,23 @@ def unrope(B=16, N=4101):
     print(f"qkv_unrope B={B} N={N}: {t * 1e6:8.1f} us  {nbytes / t / 1e12:6.2f} TB/s")
 
 
+def vit_bwd(M=16 * 4101, D=768):
+    """LayerNorm backward (bf16 dy, f32 x / dres / dx) and LayerScale backward at the C3 shape;
+    S3OD_LN_RPB / S3OD_LS_RPB select rows per block."""
+    dy = torch.randn(M, D, device="cuda").bfloat16()
+    x = torch.randn(M, D, device="cuda"); dres = torch.randn_like(x); dx = torch.empty_like(x)
+    mean = x.mean(1); rstd = torch.ones(M, device="cuda"); w = torch.ones(D, device="cuda")
+    dw, db = torch.zeros(D, device="cuda"), torch.zeros(D, device="cuda")
+    ws = torch.empty(32 * 2 * D, device="cuda")
+    t = timeit(lambda: lib()("s3od_layernorm_bwd", BF16, dy, x, mean, rstd, w, dres, dx, dw, db, ws, M, D, stream()))
+    nb = M * D * (2 + 4 + 4 + 4)
+    print(f"layernorm_bwd M={M} D={D}: {t * 1e6:8.1f} us  {nb / t / 1e12:6.2f} TB/s")
+    u = torch.randn(M, D, device="cuda").bfloat16(); du = torch.empty_like(u)
+    t = timeit(lambda: lib()("s3od_layerscale_bwd", BF16, x, u, w, du, dw, db, ws, M, D, stream()))
+    nb = M * D * (4 + 2 + 2)
+    print(f"layerscale_bwd M={M} D={D}: {t * 1e6:8.1f} us  {nb / t / 1e12:6.2f} TB/s")
+
+
 def copy(n=1 << 28):
     a = torch.empty(n, device="cuda", dtype=torch.bfloat16)
     b = torch.empty_like(a)
@@ -45,6 +62,9 @@ def copy(n=1 << 28):
 
 
 if __name__ == "__main__":
+    if sys.argv[1:] == ["vit"]:
+        vit_bwd()
+        sys.exit(0)
     copy()
     bn_bwd(relu=True)
     bn_bwd(relu=False)
