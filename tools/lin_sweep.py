@@ -106,6 +106,11 @@ def report(name, fl, t):
 
 
 if __name__ == "__main__":
+    if os.environ.get("SWEEP") == "conv256":
+        for hh in (256, 128, 64):
+            conv(f"conv fwd 256->256 3x3 @{hh}^2 bs16", 16, hh, 256, 256)
+            dgrad_conv(f"conv dgrad 256<-256 3x3 @{hh}^2 bs16", 16, hh, 256, 256)
+        sys.exit(0)
     if os.environ.get("SWEEP") == "conv64":
         conv("conv fwd 64->64 3x3 @1024^2 bs16 relu", 16, 1024, 64, 64, act=1)
         heads("mask heads fwd 64->96 (+relu+1x1) @1024^2 bs16", 16, 1024)
