@@ -24,6 +24,21 @@ def bn_bwd(npix=16 * 256 * 256, C=256, relu=True):
     print(f"bn_bwd npix={npix} C={C} relu={relu}: {t * 1e6:8.1f} us  {nbytes / t / 1e12:6.2f} TB/s (reduce+apply bytes)")
 
 
+def bn_relu_bwd(npix=16 * 256 * 256, C=256):
+    """BN + ReLU backward with the ReLU mask recomputed from z (s3od_bn_relu_bwd)."""
+    dy = torch.randn(npix, C, device="cuda").bfloat16()
+    z = torch.randn_like(dy)
+    mean = torch.zeros(C, device="cuda"); rstd = torch.ones(C, device="cuda"); w = torch.ones(C, device="cuda")
+    sc, sh = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
+    sums = torch.empty(32 * 3 * C, dtype=torch.float64, device="cuda")
+    dz = torch.empty_like(dy)
+    dw, db, dcb = (torch.zeros(C, device="cuda") for _ in range(3))
+    f = lambda: lib()("s3od_bn_relu_bwd", BF16, dy, z, sc, sh, mean, rstd, w, sums, dz, dw, db, dcb, npix, C, stream())
+    t = timeit(f)
+    nbytes = npix * C * 2 * 5
+    print(f"bn_relu_bwd npix={npix} C={C}: {t * 1e6:8.1f} us  {nbytes / t / 1e12:6.2f} TB/s (reduce+apply bytes)")
+
+
 def unrope(B=16, N=4101):
     dq = torch.randn(B * 12, N, 64, device="cuda").bfloat16()
     dk, dv = torch.randn_like(dq), torch.randn_like(dq)
@@ -62,6 +77,11 @@ def copy(n=1 << 28):
 
 
 if __name__ == "__main__":
+    if sys.argv[1:] == ["bn"]:
+        for npix in (16 * 256 * 256, 16 * 128 * 128, 16 * 64 * 64):
+            bn_bwd(npix, relu=False)
+            bn_relu_bwd(npix)
+        sys.exit(0)
     if sys.argv[1:] == ["vit"]:
         vit_bwd()
         sys.exit(0)
