@@ -586,9 +586,11 @@ static int bn_bwd_impl(int dtype, const void* dy, const void* z, const void* y_r
   S3OD_REQUIRE(C % 8 == 0 && 256 % (C / 8) == 0, "bn_bwd: C");
   hipStream_t st = (hipStream_t)stream;
   (void)hipMemsetAsync(sums, 0, sizeof(double) * S3OD_NREP * 3 * C, st);
-  // ~512 blocks for large maps (measured optimum: fewer starve HBM, more pay atomics), >= 64 pixels per block
+  // blocks per pass (tools/hbm_bench.py bn, bs 16 x 256 channels): 1024 for >= 256K pixels (1M: 606 -> 542 us,
+  // 256K: 173 -> 150 us), 512 below (64K: 1024 blocks of 64 pixels pay more in atomics: 61 -> 82 us)
   const int rows = 256 / (C / 8);
-  long ppb = max(64L, npix / dev_knob("S3OD_BN_BLOCKS", 512));
+  static const int nb_knob = dev_knob("S3OD_BN_BLOCKS", 0);
+  long ppb = max(64L, npix / (nb_knob > 0 ? nb_knob : (npix >= 262144 ? 1024 : 512)));
   ppb = (ppb + rows - 1) / rows * rows;
   const int nb = cdiv(npix, ppb);
   DISPATCH_T(dtype, {
