@@ -14,9 +14,11 @@ pass) is timed live with HIP events on its launch stream around every call insid
 `breakdown`: per-class table (GEMM / attention / memory-bound) from a separate 2-step pass with every
 entry timed, plus the whole-step MFMA fraction and the ViT-encoder ("attention block") fraction.
 `cpu_baseline`: the oracle (oracle/s3od_oracle.py, the reference's CPU fp32 path restated) on this
-host's cores (rank 0, N=1 only): 1 warm-up + --cpu-iters (2) timed iterations of one image (BASELINE.md
-"CPU-baseline plan" asks for >= 3; 2 keeps the default run within a few minutes on the box's 16-thread
-share); C2 / C5 baselines ride in the `infer` / `infer_2048` objects (C5: one timed 2048^2 image, ~90 s).
+host's cores (rank 0, N=1 only): 1 warm-up + --cpu-iters (3) timed iterations of one image (BASELINE.md
+"CPU-baseline plan": 1 + >= 3), for the train step and for C2 (the `infer` object); the C5 baseline in
+`infer_2048` is one timed 2048^2 image without warm-up (~80 s of CPU per image on the box's share).
+Attention backward work follows SURVEY §8(d) (8*N^2*64 per (b,h), recompute not counted); the roofline
+object also carries the executed figure (14*N^2*64) for that entry.
 """
 from __future__ import annotations
 
@@ -253,6 +255,23 @@ def spawn_ranks(n):
     return subprocess.call(cmd, env=env)
 
 
+def dry_run(args, world, rank, local):
+    """`--dry-run`: the rank layout the timed run would use, checked without a GPU — every rank joins a
+    gloo group and all-reduces (rank, local rank, per-rank batch); rank 0 prints one JSON line."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    B = args.batch or (16 if args.mode == "train" else 8)
+    t = torch.tensor([float(rank), float(local), float(B), 1.0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "world_size": world, "gpus_requested": args.gpus, "rank_sum": int(t[0]),
+                          "local_rank_sum": int(t[1]), "global_batch": int(t[2]), "ranks_joined": int(t[3]),
+                          "parallelism": f"dp{world}"}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -263,11 +282,13 @@ def main():
     ap.add_argument("--size", type=int, default=1024)
     ap.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-iters", type=int, default=2, help="timed CPU-baseline iterations (after 1 warm-up)")
+    ap.add_argument("--cpu-iters", type=int, default=3, help="timed CPU-baseline iterations (after 1 warm-up)")
     ap.add_argument("--no-infer", action="store_true", help="skip the secondary inference lines (train mode)")
     ap.add_argument("--no-breakdown", action="store_true", help="skip the per-class profiling pass")
     ap.add_argument("--ddp", action="store_true",
                     help="use the RCCL data-parallel path even at world size 1 (rehearsal on one GPU)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch path only: spawn / join the ranks over gloo (no GPU call), rank 0 reports the world")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -278,6 +299,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus > 1 and world != args.gpus and rank == 0:
         print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; using the launcher's world size", file=sys.stderr)
+    if args.dry_run:
+        return dry_run(args, world, rank, local)
     use_dist = world > 1 or args.ddp
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -387,6 +410,11 @@ def main():
             "mfma_frac_step": round(value / world * per_img / peak, 4) if per_img else None,
             "finite": ok,
         }
+        if dom.startswith("s3od_attn_bwd") and kms > 0:
+            # what the kernels issue: S recomputed in the dK/dV pass, S and dP again in the dQ pass
+            ex = work * 14.0 / 8.0
+            res["roofline"]["executed_work_per_launch"] = ex
+            res["roofline"]["executed_frac"] = round(ex / (kms * 1e-3) / pk, 4)
         if bd is not None:
             res["breakdown"] = bd
         if args.mode == "train" and world == 1 and not args.no_infer and args.dtype == "bf16":

@@ -65,48 +65,56 @@ __global__ void canvas_fill_kernel(float* out, int S) {
 }
 
 // ---------------------------------------------------------------- antialiased bilinear
-// PyTorch _upsample_bilinear2d_aa weights for output index i (align_corners=False)
-DEV int aa_weights(int i, int in, int out, float* w, int maxw) {
-  float scale = (float)in / (float)out;
-  float support = scale >= 1.f ? scale : 1.f;
-  float center = scale * (i + 0.5f);
-  float invscale = scale >= 1.f ? 1.f / scale : 1.f;
-  int xmin = max((int)(center - support + 0.5f), 0);
-  int xsize = min((int)(center + support + 0.5f), in) - xmin;
-  if (xsize > maxw) xsize = maxw;
-  float tot = 0.f;
-  for (int j = 0; j < xsize; j++) {
-    float x = (j + xmin - center + 0.5f) * invscale;
-    float ww = fabsf(x) < 1.f ? 1.f - fabsf(x) : 0.f;
-    w[j] = ww; tot += ww;
-  }
-  for (int j = 0; j < xsize; j++) w[j] = tot != 0.f ? w[j] / tot : 0.f;
-  return xmin | (xsize << 20);
+// PyTorch _upsample_bilinear2d_aa taps for output index i (align_corners=False, triangle filter with
+// support max(scale, 1)).  The taps are not buffered: the span [xmin, xmin + xsize) is derived here and
+// each weight is recomputed where it is used, so any downscale factor works (the reference resizes back
+// to any original size, predictor.py:118-124).
+struct AASpan {
+  int xmin, xsize;
+  float center, invscale, tot;
+};
+
+DEV float aa_tap(const AASpan& s, int j) {
+  float x = (j + s.xmin - s.center + 0.5f) * s.invscale;
+  return fabsf(x) < 1.f ? 1.f - fabsf(x) : 0.f;
 }
 
-// pass 1: sigmoid + crop + horizontal resample: [3][LH][LW] logits -> tmp [3][h][W0]
+DEV AASpan aa_span(int i, int in, int out) {
+  AASpan s;
+  float scale = (float)in / (float)out;
+  float support = scale >= 1.f ? scale : 1.f;
+  s.center = scale * (i + 0.5f);
+  s.invscale = scale >= 1.f ? 1.f / scale : 1.f;
+  s.xmin = max((int)(s.center - support + 0.5f), 0);
+  s.xsize = min((int)(s.center + support + 0.5f), in) - s.xmin;
+  float tot = 0.f;
+  for (int j = 0; j < s.xsize; j++) tot += aa_tap(s, j);
+  s.tot = tot;                // weights are w_j / tot (0 when tot == 0), as PyTorch normalises them
+  return s;
+}
+
+DEV float aa_weight(const AASpan& s, int j) { return s.tot != 0.f ? aa_tap(s, j) / s.tot : 0.f; }
+
+// pass 1: sigmoid + crop + horizontal resample: [NM][LH][LW] logits -> tmp [NM][h][W0]
 __global__ void post_h_kernel(const float* __restrict__ logits, int LH, int LW, int pad_h, int pad_w, int h, int w, int W0,
                               float* __restrict__ tmp) {
   int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, c = blockIdx.z;
   if (x >= W0) return;
-  float wt[64];
-  int r = aa_weights(x, w, W0, wt, 64);
-  int xmin = r & 0xFFFFF, xs = r >> 20;
-  const float* row = logits + ((long)c * LH + (pad_h + y)) * LW + pad_w;
+  AASpan sp = aa_span(x, w, W0);
+  const float* row = logits + ((long)c * LH + (pad_h + y)) * LW + pad_w + sp.xmin;
   float acc = 0.f;
-  for (int j = 0; j < xs; j++) acc += wt[j] * (1.f / (1.f + expf(-row[xmin + j])));
+  for (int j = 0; j < sp.xsize; j++) acc += aa_weight(sp, j) * (1.f / (1.f + expf(-row[j])));
   tmp[((long)c * h + y) * W0 + x] = acc;
 }
 
-// pass 2: vertical resample -> out [3][H0][W0]
+// pass 2: vertical resample -> out [NM][H0][W0]
 __global__ void post_v_kernel(const float* __restrict__ tmp, int h, int H0, int W0, float* __restrict__ out) {
   int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, c = blockIdx.z;
   if (x >= W0) return;
-  float wt[64];
-  int r = aa_weights(y, h, H0, wt, 64);
-  int ymin = r & 0xFFFFF, ys = r >> 20;
+  AASpan sp = aa_span(y, h, H0);
+  const float* col = tmp + ((long)c * h + sp.xmin) * W0 + x;
   float acc = 0.f;
-  for (int j = 0; j < ys; j++) acc += wt[j] * tmp[((long)c * h + ymin + j) * W0 + x];
+  for (int j = 0; j < sp.xsize; j++) acc += aa_weight(sp, j) * col[(long)j * W0];
   out[((long)c * H0 + y) * W0 + x] = acc;
 }
 
@@ -127,7 +135,7 @@ int s3od_preprocess(const void* img, int H0, int W0, int new_h, int new_w, int p
 int s3od_sigmoid_unpad_resize(const float* logits, int NM, int LH, int LW, int pad_h, int pad_w, int h, int w, int H0, int W0,
                               float* tmp, float* out, void* stream) {
   S3OD_REQUIRE(NM >= 1 && NM <= 64 && h > 0 && w > 0, "postprocess: bad mask count / crop");
-  S3OD_REQUIRE((float)w / W0 < 32.f && (float)h / H0 < 32.f, "postprocess: downscale factor too large");
+  S3OD_REQUIRE(H0 > 0 && W0 > 0 && H0 <= 65535 && h <= 65535, "postprocess: output size out of range");
   S3OD_REQUIRE(pad_h + h <= LH && pad_w + w <= LW, "postprocess: crop outside the logits");
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(post_h_kernel, dim3(cdiv(W0, 256), h, NM), dim3(256), 0, st, logits, LH, LW, pad_h, pad_w, h, w, W0, tmp);

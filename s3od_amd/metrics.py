@@ -127,6 +127,22 @@ def find_gt_mask_path(image_path: str, data_dir: str) -> Optional[str]:
     return None
 
 
+def read_gray_u8(path):
+    """``cv2.imread(path, cv2.IMREAD_GRAYSCALE)`` restated on PIL: 16-bit masks are scaled to 8 bits
+    (>> 8, as cv2 does; PIL's convert("L") would clip them) and colour masks use cv2's BT.601
+    fixed-point weights ((4899 R + 9617 G + 1868 B + 8192) >> 14).  Remaining gap (unpinned, cv2 is
+    absent): JPEG masks, which libjpeg converts to grey inside the decoder."""
+    from PIL import Image
+    im = Image.open(path)
+    if im.mode in ("I;16", "I;16B", "I;16L", "I"):
+        a = np.asarray(im).astype(np.int64)
+        return np.clip(a >> 8, 0, 255).astype(np.uint8)
+    if im.mode in ("L", "1"):
+        return np.asarray(im.convert("L"))
+    a = np.asarray(im.convert("RGB")).astype(np.int64)
+    return ((4899 * a[..., 0] + 9617 * a[..., 1] + 1868 * a[..., 2] + 8192) >> 14).astype(np.uint8)
+
+
 def process_dataset(data_dir: str, predictor, compute_best_metrics: bool = False):
     """compute_metrics.py:42-100: predict every ``images/*`` file, score it against ``masks/``.
 
@@ -145,7 +161,7 @@ def process_dataset(data_dir: str, predictor, compute_best_metrics: bool = False
         if not gt_path:
             print(f"Warning: GT mask not found for {image_path}")
             continue
-        gt_mask = (np.asarray(Image.open(gt_path).convert("L")) > 128).astype(np.float32)
+        gt_mask = (read_gray_u8(gt_path) > 128).astype(np.float32)
         gt_t = torch.from_numpy(gt_mask).cuda()
         soft = torch.as_tensor(result.soft_mask)
         counter.step(soft, gt_t.clone())

@@ -265,7 +265,9 @@ def fit(config, train_loader=None, val_loader=None, augment=None, val_augment=No
             ck = load_checkpoint(ckpt_path, module, optimizer=opt, scheduler=sched)
             start_epoch = int(ck.get("epoch", 0)) + 1
             global_step = int(ck.get("global_step", 0))
-    name = ts.get("experiment_name", "s3od")
+    # get_experiment_name (train.py:58-69): <experiment_name>_<timestamp>, so a second run with the same
+    # name never mixes its top-k files with an earlier run's; rank 0 (the only writer) picks the stamp
+    name = experiment_dir_name(ts.get("experiment_name", "s3od"))
     topk = TopK(Path(ts.get("save_dir", "checkpoints")) / name, monitor="val_dice_epoch", mode="max", k=3, save_last=True)
     es_cfg = ts.get("early_stopping")
     stopper = EarlyStop(**es_cfg) if es_cfg else None
@@ -277,8 +279,7 @@ def fit(config, train_loader=None, val_loader=None, augment=None, val_augment=No
     bad = torch.zeros((), dtype=torch.int32, device=dev)
 
     def check_finite(where):
-        if int(bad) > 0:
-            raise FloatingPointError(f"non-finite training loss ({int(bad)} micro-batches) before {where}")
+        nan_guard(bad, world, where)
     for epoch in range(start_epoch, max_epochs):
         module.current_epoch_ = epoch
         if hasattr(train_loader, "sampler") and hasattr(train_loader.sampler, "set_epoch"):
@@ -333,6 +334,26 @@ def fit(config, train_loader=None, val_loader=None, augment=None, val_augment=No
             "history": history, "module": module, "optimizer": opt, "scheduler": sched, "evaluation": evaluation}
 
 
+def experiment_dir_name(base, now=None):
+    """get_experiment_name (train.py:58-69): ``f"{base}_{%Y%m%d_%H%M%S}"``."""
+    import datetime
+    return f"{base}_{(now or datetime.datetime.now()).strftime('%Y%m%d_%H%M%S')}"
+
+
+def nan_guard(bad, world, where, group=None):
+    """Raise FloatingPointError when any rank counted a non-finite loss.  The per-rank counter is
+    MAX-all-reduced first, so every rank takes the same raise/continue decision at the same step (a
+    rank raising alone would leave its peers blocked in the next collective until the timeout)."""
+    if world > 1:
+        flag = bad.clone()
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    else:
+        flag = bad
+    n = int(flag)
+    if n > 0:
+        raise FloatingPointError(f"non-finite training loss ({n} micro-batches on the worst rank) before {where}")
+
+
 def rccl_timeout():
     """Collective timeout (S3OD_RCCL_TIMEOUT_S, default 30 min, as torch.distributed's default)."""
     import datetime
@@ -353,12 +374,38 @@ def evaluate(ev, best_model_path, log=print):
     return out
 
 
+def dry_run(cfg):
+    """The launch path without a GPU: every rank joins a gloo group, the ranks all-reduce their rank ids and
+    their DistributedSampler shard sizes, and rank 0 prints one JSON line (world size, devices requested)."""
+    import json
+    from torch.utils.data.distributed import DistributedSampler
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", timeout=rccl_timeout())
+    bs = int(cfg["dataset"].get("train_batch_size", 1))
+    n = 10 * bs * max(world, 1) + 3                              # a ragged synthetic dataset length
+    shard = len(DistributedSampler(range(n), num_replicas=world, rank=rank, shuffle=True, drop_last=True))
+    t = torch.tensor([float(rank), float(shard), 1.0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "world_size": world, "devices": int(cfg["backend"].get("devices", 1)),
+                          "rank_sum": int(t[0]), "samples_per_epoch": int(t[1]), "ranks_joined": int(t[2]),
+                          "accumulate_grad_batches": int(cfg["backend"].get("accumulate_grad_batches", 1))}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
 def main(argv=None):
     """``python -m s3od_amd.train --config-dir <synth_sod/.../config> backend=8gpu dataset=synth ...``"""
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--config-dir", required=True)
     ap.add_argument("--config-name", default="train")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="spawn the ranks and join a gloo group (no GPU call), report the world from rank 0, exit")
     ap.add_argument("overrides", nargs="*")
     args = ap.parse_args(argv)
     cfg = compose_config(args.config_dir, args.overrides, args.config_name)
@@ -370,6 +417,8 @@ def main(argv=None):
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={devices}",
                "--master-addr=127.0.0.1", f"--master-port={port}", "-m", "s3od_amd.train"] + list(argv or sys.argv[1:])
         return subprocess.call(cmd)
+    if args.dry_run:
+        return dry_run(cfg)
     out = fit(cfg)
     print({k: v for k, v in out.items() if k in ("epochs", "global_step", "best_model_path")})
     return 0

@@ -129,3 +129,36 @@ def test_bucket_ranges_partition_grad_params():
     unused = set(m.unused_parameter_names())
     assert not unused & set(names)
     assert set(names) | unused == {n for n, _ in m.named_parameters()}
+
+
+def _worker_nan(rank, world, port, q):
+    """Only rank 1 counted a non-finite loss: both ranks must raise at the same check."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from s3od_amd.train import nan_guard
+        clean = torch.zeros((), dtype=torch.int32)
+        nan_guard(clean, world, "step 0")                     # nobody saw a NaN: no raise anywhere
+        bad = torch.tensor(1 if rank == 1 else 0, dtype=torch.int32)
+        try:
+            nan_guard(bad, world, "step 1")
+            raised = False
+        except FloatingPointError:
+            raised = True
+        dist.barrier()                                        # both ranks are still in lock-step
+        q.put((rank, raised))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_nan_guard_all_ranks_raise_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_nan, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}

@@ -54,25 +54,46 @@ def test_fixture_strict(br):
 
 
 def test_fixture_bf16(br):
+    """bf16 on the fixture: best_idx bit-exact; mask IoU vs the reference's sign bits, with the flip band
+    SURVEY §8(c) asks for (the fraction of pixels whose strict logit |l| < 2·max|Δ_bf16|: IoU >= 0.999 only
+    means something when that band is < 1e-3; with the synthetic weights most logits sit near 0).  The
+    strict f32 logits stand in for the reference's values (pinned above: sign IoU >= 0.999, ≤ 1e-4 on
+    the mask).  The numbers are written to gpurun_out/bf16_fixture_iou.json when that directory exists."""
+    import json
+    import os
     g = np.load(GOLDEN / "fixture_1024.npz")
     img = Image.open(FIXTURE / "image.jpg").convert("RGB")
+    x, _ = br._preprocess(np.array(img))
+    with torch.no_grad():
+        l32 = br.model(x)["pred_masks"][0].float().cpu().numpy()
     br.model.compute_dtype = "bf16"
     try:
         res = br.remove_background(img)
-        x, _ = br._preprocess(np.array(img))
         with torch.no_grad():
             lg = br.model(x)["pred_masks"][0].float().cpu().numpy()
     finally:
         br.model.compute_dtype = "f32"
     ref_bits = np.unpackbits(g["mask_pos_bits"])[: lg.size].astype(bool).reshape(lg.shape)
     m_iou = iou(lg > 0, ref_bits)
-    best = res.all_masks[int(g["best_idx"])] > 0.5
-    print(f"bf16 fixture: mask IoU vs reference {m_iou:.5f}, best_idx {res.all_ious.argmax()} (ref {int(g['best_idx'])})")
+    d = np.abs(lg - l32)
+    maxd = float(d.max())
+    band = float((np.abs(l32) < 2 * maxd).mean())
+    outside = np.abs(l32) >= 2 * maxd
+    rec = {"mask_iou_vs_reference": m_iou, "mask_iou_vs_strict": iou(lg > 0, l32 > 0),
+           "max_abs_logit_diff": maxd, "rel_l2_logits": float(np.linalg.norm(lg - l32) / np.linalg.norm(l32)),
+           "flip_band_fraction": band, "sign_agreement_outside_band": float(((lg > 0) == (l32 > 0))[outside].mean()),
+           "median_abs_logit": float(np.median(np.abs(l32))), "best_idx": int(res.all_ious.argmax()),
+           "best_idx_ref": int(g["best_idx"]),
+           "note": "synthetic weights (real ones are not available offline); strict f32 logits stand in for the reference's"}
+    print("bf16 fixture:", json.dumps(rec))
+    if os.path.isdir("gpurun_out"):
+        json.dump(rec, open("gpurun_out/bf16_fixture_iou.json", "w"), indent=1)
     assert int(res.all_ious.argmax()) == int(g["best_idx"])
+    assert rec["sign_agreement_outside_band"] == 1.0
     assert m_iou >= 0.99
 
 
-@pytest.mark.parametrize("shape", [(100, 100), (400, 800), (800, 400), (2000, 2000), (480, 640)])
+@pytest.mark.parametrize("shape", [(100, 100), (400, 800), (800, 400), (2000, 2000), (480, 640), (20, 30), (31, 31), (40, 4000)])
 def test_output_shape_matches_input(br, shape):
     """tests/test_inference_package.py:49-122 (shape contract; resize parity unpinned: cv2 absent)."""
     rng = np.random.default_rng(0)

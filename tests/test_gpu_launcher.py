@@ -61,7 +61,9 @@ def test_fit_two_epochs_accumulate_and_resume(tmp_path):
     # LinearLR(1.0 -> 1.0, 1 epoch) then cosine: the lr moved after the second epoch only
     assert h[0]["lr"] == pytest.approx([1e-5, 1e-4])
     assert h[1]["lr"][0] < 1e-5
-    d = tmp_path / "ckpt" / "t"
+    from pathlib import Path
+    d = Path(out["best_model_path"]).parent            # <save_dir>/<experiment_name>_<timestamp> (train.py:58-69,101)
+    assert d.parent == tmp_path / "ckpt" and d.name.startswith("t_") and len(d.name) == len("t_20260101_000000")
     assert (d / "last.ckpt").exists()
     top = sorted(p.name for p in d.glob("epoch=*-val_dice_epoch=*.ckpt"))
     assert len(top) == 2 and out["best_model_path"] is not None

@@ -112,7 +112,7 @@ def test_train_mode_forward_under_no_grad():
     assert n == 28
 
 
-@pytest.mark.parametrize("hw", [(480, 640), (2000, 2000), (800, 400)])
+@pytest.mark.parametrize("hw", [(480, 640), (2000, 2000), (800, 400), (20, 30), (31, 31), (40, 4000), (4000, 40), (1, 1)])
 def test_postprocess_antialias_resize(hw):
     from s3od_amd._lib import lib, stream
     from oracle.s3od_oracle import get_pad_info

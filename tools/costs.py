@@ -5,8 +5,10 @@ the call's own arguments (include/s3od_hip.h), i.e. the work the reference's op 
 
 * GEMM-shaped entries: 2*M*N*K of the op they implement (a conv's dgrad / wgrad count the same
   2*B*OH*OW*Cout*Cin*KH*KW as its forward; ConvTranspose forward is a conv dgrad with the conv-view
-  grid, so the same formula holds).  Attention forward 4*N^2*64 per (b,h) (QK^T + PV); backward the
-  FlashAttention convention 2.5x forward (= 10*N^2*64, recompute of S included).
+  grid, so the same formula holds).  Attention forward 4*N^2*64 per (b,h) (QK^T + PV); backward
+  SURVEY §8(d)'s convention (training = 3x forward, "flash recompute is not counted"): 2x forward =
+  8*N^2*64 (dV = P^T dO, dP = dO V^T, dQ = dS K, dK = dS^T Q).  ``executed(name, args)`` gives what the
+  kernels actually issue (14*N^2*64: S in the dK/dV pass, S and dP again in the dQ pass).
 * memory-bound entries: mandatory bytes in + out at the storage dtype (each tensor touched once).
 """
 from __future__ import annotations
@@ -44,10 +46,10 @@ def cost(name, a):
         return "mfma", 4.0 * B * H * N * N * 64
     if n == "attn_bwd":
         B, H, N = a[11:14]
-        return "mfma", 10.0 * B * H * N * N * 64
+        return "mfma", 8.0 * B * H * N * N * 64
     if n == "attn_bwd_qkv":
         B, H, N = a[15:18]
-        return "mfma", 10.0 * B * H * N * N * 64
+        return "mfma", 8.0 * B * H * N * N * 64
     # ---- memory-bound
     if n == "layernorm_fwd":
         dt, M = a[0], a[7]
@@ -103,6 +105,18 @@ def cost(name, a):
         total = int(sizes.sum()) if hasattr(sizes, "sum") else 0
         return "hbm", 28.0 * total      # read p, g, m, v; write p, m, v (fp32)
     return "other", 0.0
+
+
+def executed(name, a):
+    """MFMA FLOPs the kernels issue, where that differs from the algorithmic figure (else None)."""
+    n = name[len("s3od_"):]
+    if n == "attn_bwd":
+        B, H, N = a[11:14]
+        return 14.0 * B * H * N * N * 64
+    if n == "attn_bwd_qkv":
+        B, H, N = a[15:18]
+        return 14.0 * B * H * N * N * 64
+    return None
 
 
 CLASS = {
