@@ -760,6 +760,321 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(const T* __restrict__ 
   }
 }
 
+// ===================================================================================== backward, bf16, 32x32x16
+// The bf16 backward on v_mfma_f32_32x32x16_bf16: an MFMA of this shape holds the SIMD's vector issue for 8 of
+// its 32 cycles (16x16x32: 8 of 16), so per multiply-add it leaves 1.5x the VALU issue room for the softmax
+// recompute (exp2, P*(dP - delta), two bf16 packs per score), which is what bounds the 16x16x32 kernels above
+// (PMC: ~2.7 VALU per MFMA, 22 % MFMA-busy).  Same algorithm and register-operand tricks:
+//   dK/dV pass (one wave = 32 keys):  S = Q K^T, dP = dO V^T with the key on the lane (B = K / V fragments in
+//     registers, A = Q / dO rows from LDS, C = -LSE / -delta rows); P and dS are then, as they stand in the
+//     accumulators, the A operands of dV = P^T dO and dK = dS^T Q, whose B operands (dO, Q with the query on
+//     the k index) come from transposed LDS reads of the same images.
+//   dQ pass (one wave = 32 queries): S^T = K Q^T, dP^T = V dO^T with the query on the lane (C = -LSE / -delta
+//     of the lane's query: constant register blocks, no per-tile init), dQ = dS K (A = dS^T accumulators,
+//     B = K by transposed reads).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+namespace {
+DEV f32x16 mma32(bf16x8 a, bf16x8 b, f32x16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0); }
+
+// 64-row x 64-col bf16 image, 128-B rows; 16-B chunk ch of row r at r*128 + 16*(ch ^ sw(r)) with
+// sw(r) = ((r>>1)&1)<<2 | ((r>>2)&3): conflict-free for the 32x32x16 A-operand row reads (ds_read_b128, rows
+// r0 + lane&31 in the b128 lane groups) AND the transposed B-operand reads (ds_read_b64_tr_b16: per 32-lane
+// half 4 rows x 32 columns; rows 4m and 4m+2 land in chunk sets that differ in bit 2)
+struct Img32 {
+  static constexpr int BYTES = 64 * 128;
+  DEV static int sw(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+  DEV static int at(int row, int byte) { return row * 128 + ((((byte >> 4) ^ sw(row)) << 4) | (byte & 15)); }
+};
+// A fragment of rows r0..r0+31, k-step ks (16 columns): lane (r = lane&31, h = lane>>5) gets X[r0+r][16ks+8h .. +7]
+DEV bf16x8 row32(const char* img, int r0, int ks, int lane) {
+  return *(const bf16x8*)(img + Img32::at(r0 + (lane & 31), ks * 32 + (lane >> 5) * 16));
+}
+// B fragment (k = rows, column on the lane) of rows r0..r0+15 in the 32x32x16 accumulator k order:
+// element j of lane half h = row r0 + 8(j>>2) + 4h + (j&3), column c0 + (lane&31)
+DEV bf16x8 tr32(const char* img, int r0, int c0, int lane) {
+  const int h = lane >> 5, g16 = (lane >> 4) & 1, li = lane & 15, q = li >> 2, p = li & 3;
+  const int byte = (c0 + 16 * g16 + 4 * p) * 2;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + Img32::at(r0 + 4 * h + q, byte)));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + Img32::at(r0 + 8 + 4 * h + q, byte)));
+  bf16x4 a = __builtin_bit_cast(bf16x4, lo), b = __builtin_bit_cast(bf16x4, hi);
+  return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+// accumulator registers 8s .. 8s+7 as a bf16 operand fragment (k-step s of the row index)
+DEV bf16x8 pack_acc(const f32x16& x, int s) {
+  return bf16x8{(bf16)x[8 * s + 0], (bf16)x[8 * s + 1], (bf16)x[8 * s + 2], (bf16)x[8 * s + 3],
+                (bf16)x[8 * s + 4], (bf16)x[8 * s + 5], (bf16)x[8 * s + 6], (bf16)x[8 * s + 7]};
+}
+// row of accumulator register i of lane half h (32x32 C/D layout)
+DEV int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+// stage a [64 rows][64] bf16 tile (row stride ld) through registers into an Img32, NT threads
+template <int NT> struct RowTile32 {
+  static constexpr int CH = 512 / NT;     // 16-B chunks per thread
+  uint4 r[CH];
+  DEV void load(const bf16* base, long ld, int row0, int N, int tid) {
+#pragma unroll
+    for (int i = 0; i < CH; i++) {
+      const int c = tid + NT * i, row = row0 + (c >> 3), col = (c & 7) * 8;
+      r[i] = row < N ? *(const uint4*)(base + (long)row * ld + col) : make_uint4(0, 0, 0, 0);
+    }
+  }
+  DEV void store(char* lds, int tid) {
+#pragma unroll
+    for (int i = 0; i < CH; i++) {
+      const int c = tid + NT * i;
+      *(uint4*)(lds + Img32::at(c >> 3, (c & 7) * 16)) = r[i];
+    }
+  }
+};
+
+// fused epilogue of one wave's 32-row x 64-d result (rows tok0 + acc_row, column d = 32 db + lane&31) into
+// d_qkv (inverse RoPE on the patch tokens of q / k, `scale`), with the column sums for the q / v bias
+template <typename T>
+DEV void qkv_sink32(const QkvSink& o, int which, int b, int hh, int H, int tok0, int N, int lane, const f32x16 (&val)[2],
+                    float scale, float (&csum)[2]) {
+  const int h = lane >> 5, c = lane & 31;
+  T* base = (T*)o.dqkv + (long)which * H * 64 + hh * 64;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int tok = tok0 + acc_row(i, h);
+    if (tok >= N) continue;
+    float out[2] = {val[0][i] * scale, val[1][i] * scale};
+    if (which < 2 && tok >= N - o.P) {
+      const int tp = tok - (N - o.P);
+      const float* cs = o.cs + (long)tp * 64;
+      const float* sn = o.sn + (long)tp * 64;
+      out[0] = (cs[c] * val[0][i] + sn[c + 32] * val[1][i]) * scale;
+      out[1] = (cs[c + 32] * val[1][i] - sn[c] * val[0][i]) * scale;
+    }
+    T* row = base + ((long)b * N + tok) * (3L * H * 64);
+#pragma unroll
+    for (int db = 0; db < 2; db++) {
+      row[32 * db + c] = from_f<T>(out[db]);
+      csum[db] += out[db];
+    }
+  }
+}
+DEV void qkv_colsum32(const QkvSink& o, int which, int hh, int H, int rep, int lane, float (&csum)[2]) {
+  const int D = H * 64;
+#pragma unroll
+  for (int db = 0; db < 2; db++) {
+    const float v = csum[db] + __shfl_xor(csum[db], 32);
+    if (lane < 32) atomicAdd(o.ws + (long)rep * 2 * D + (which == 0 ? 0 : D) + hh * 64 + 32 * db + lane, v);
+  }
+}
+}  // namespace
+
+// dK, dV.  Workgroup = W waves x 32 keys of one (b,h); loop over 64-query tiles (Q, dO, -LSE, -delta staged
+// in double-buffered LDS, one barrier per tile).
+template <int W>
+__global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
+                                                                   const bf16* __restrict__ V, const bf16* __restrict__ dO,
+                                                                   const float* __restrict__ LSE, const float* __restrict__ Dl,
+                                                                   bf16* __restrict__ dK, bf16* __restrict__ dV, int N, int H,
+                                                                   QkvSink sink) {
+  constexpr int NT = 64 * W, SB = 2 * Img32::BYTES + 512;
+  __shared__ __attribute__((aligned(16))) char smem[2 * SB];
+  const int bh = blockIdx.y, b = bh / H, hh = bh - b * H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const bf16* Qp = Q + (long)bh * N * 64;
+  const bf16* dOp = dO + (long)b * N * (H * 64) + hh * 64;
+  const long ldo = (long)H * 64;
+  const float* Lp = LSE + (long)bh * N;
+  const float* Dp = Dl + (long)bh * N;
+  const int k0 = blockIdx.x * (32 * W) + wave * 32;
+  bf16x8 kf[4], vf[4];
+  {
+    const int key = k0 + (lane & 31);
+    const bf16* kr = K + ((long)bh * N + key) * 64 + 8 * h;
+    const bf16* vr = V + ((long)bh * N + key) * 64 + 8 * h;
+    bf16x8 z; for (int e = 0; e < 8; e++) z[e] = (bf16)0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ks++) {
+      kf[ks] = key < N ? *(const bf16x8*)(kr + 16 * ks) : z;
+      vf[ks] = key < N ? *(const bf16x8*)(vr + 16 * ks) : z;
+    }
+  }
+  f32x16 dk[2], dv[2];
+#pragma unroll
+  for (int db = 0; db < 2; db++) for (int i = 0; i < 16; i++) { dk[db][i] = 0.f; dv[db][i] = 0.f; }
+  RowTile32<NT> tq, tdo;
+  float lse_r = 0.f, dl_r = 0.f;
+  const int nqt = (N + 63) / 64;
+  auto stage_load = [&](int qt) {
+    tq.load(Qp, 64, qt * 64, N, tid);
+    tdo.load(dOp, ldo, qt * 64, N, tid);
+    if (tid < 64) { const int q = qt * 64 + tid; lse_r = q < N ? -Lp[q] : -INFINITY; dl_r = q < N ? -Dp[q] : 0.f; }
+  };
+  auto stage_store = [&](char* base) {
+    tq.store(base, tid); tdo.store(base + Img32::BYTES, tid);
+    if (tid < 64) { ((float*)(base + 2 * Img32::BYTES))[tid] = lse_r; ((float*)(base + 2 * Img32::BYTES))[64 + tid] = dl_r; }
+  };
+  stage_load(0);
+  stage_store(smem);
+  __syncthreads();
+  int cur = 0;
+  for (int qt = 0; qt < nqt; qt++) {
+    const bool more = qt + 1 < nqt;
+    if (more) stage_load(qt + 1);
+    const char* qs_ = smem + cur * SB;
+    const char* dos = qs_ + Img32::BYTES;
+    const float* lsel = (const float*)(qs_ + 2 * Img32::BYTES);
+    const float* dll = lsel + 64;
+    f32x16 s[2], dp[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; qb++) {
+#pragma unroll
+      for (int m = 0; m < 4; m++) {   // C = -LSE / -delta of rows 32qb + 8m + 4h + 0..3 (broadcast reads)
+        const f32x4 nl = *(const f32x4*)(lsel + 32 * qb + 8 * m + 4 * h), nd = *(const f32x4*)(dll + 32 * qb + 8 * m + 4 * h);
+#pragma unroll
+        for (int e = 0; e < 4; e++) { s[qb][4 * m + e] = nl[e]; dp[qb][4 * m + e] = nd[e]; }
+      }
+#pragma unroll
+      for (int ks = 0; ks < 4; ks++) {
+        s[qb] = mma32(row32(qs_, 32 * qb, ks, lane), kf[ks], s[qb]);
+        dp[qb] = mma32(row32(dos, 32 * qb, ks, lane), vf[ks], dp[qb]);
+      }
+    }
+    // P = exp2(S - LSE[q]); dS = P (dP - delta[q])   (invalid q: -LSE = -inf -> P = 0)
+#pragma unroll
+    for (int qb = 0; qb < 2; qb++)
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        const float p = fexp2(s[qb][i]);
+        s[qb][i] = p;
+        dp[qb][i] *= p;
+      }
+    // dV += P^T dO ; dK += dS^T Q   (k = query: 4 steps of 16)
+#pragma unroll
+    for (int qb = 0; qb < 2; qb++)
+#pragma unroll
+      for (int st = 0; st < 2; st++) {
+        const bf16x8 pa = pack_acc(s[qb], st), da = pack_acc(dp[qb], st);
+#pragma unroll
+        for (int db = 0; db < 2; db++) {
+          dv[db] = mma32(pa, tr32(dos, 32 * qb + 16 * st, 32 * db, lane), dv[db]);
+          dk[db] = mma32(da, tr32(qs_, 32 * qb + 16 * st, 32 * db, lane), dk[db]);
+        }
+      }
+    if (more) stage_store(smem + (cur ^ 1) * SB);
+    __syncthreads();
+    cur ^= 1;
+  }
+  if (sink.dqkv) {
+    float csk[2] = {0.f, 0.f}, csv[2] = {0.f, 0.f};
+    qkv_sink32<bf16>(sink, 1, b, hh, H, k0, N, lane, dk, LN2, csk);
+    qkv_sink32<bf16>(sink, 2, b, hh, H, k0, N, lane, dv, 1.f, csv);
+    if (sink.ws) qkv_colsum32(sink, 2, hh, H, (blockIdx.y * gridDim.x + blockIdx.x) % S3OD_NREP, lane, csv);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int key = k0 + acc_row(i, h);
+    if (key >= N) continue;
+    bf16* dkr = dK + ((long)bh * N + key) * 64;
+    bf16* dvr = dV + ((long)bh * N + key) * 64;
+#pragma unroll
+    for (int db = 0; db < 2; db++) {
+      dkr[32 * db + (lane & 31)] = (bf16)(dk[db][i] * LN2);
+      dvr[32 * db + (lane & 31)] = (bf16)dv[db][i];
+    }
+  }
+}
+
+// dQ (w.r.t. the pre-scaled q).  Workgroup = W waves x 32 queries; loop over 64-key tiles.
+template <int W>
+__global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
+                                                                 const bf16* __restrict__ V, const bf16* __restrict__ dO,
+                                                                 const float* __restrict__ LSE, const float* __restrict__ Dl,
+                                                                 bf16* __restrict__ dQ, int N, int H, QkvSink sink) {
+  constexpr int NT = 64 * W, SB = 2 * Img32::BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * SB];
+  const int bh = blockIdx.y, b = bh / H, hh = bh - b * H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const bf16* Kp = K + (long)bh * N * 64;
+  const bf16* Vp = V + (long)bh * N * 64;
+  const int q0 = blockIdx.x * (32 * W) + wave * 32;
+  bf16x8 qf[4], of[4];
+  f32x16 nl, nd;     // C operands: -LSE (log2 units) / -delta of the lane's query, all 16 rows
+  {
+    const int q = q0 + (lane & 31);
+    const bf16* qr = Q + ((long)bh * N + q) * 64 + 8 * h;
+    const bf16* orow = dO + ((long)b * N + q) * (H * 64) + hh * 64 + 8 * h;
+    bf16x8 z; for (int e = 0; e < 8; e++) z[e] = (bf16)0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ks++) {
+      qf[ks] = q < N ? *(const bf16x8*)(qr + 16 * ks) : z;
+      of[ks] = q < N ? *(const bf16x8*)(orow + 16 * ks) : z;
+    }
+    const float l = q < N ? -LSE[(long)bh * N + q] : -INFINITY, d = q < N ? -Dl[(long)bh * N + q] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; i++) { nl[i] = l; nd[i] = d; }
+  }
+  f32x16 dq[2];
+#pragma unroll
+  for (int db = 0; db < 2; db++) for (int i = 0; i < 16; i++) dq[db][i] = 0.f;
+  RowTile32<NT> tk, tv;
+  const int nkt = (N + 63) / 64;
+  tk.load(Kp, 64, 0, N, tid); tv.load(Vp, 64, 0, N, tid);
+  tk.store(smem, tid); tv.store(smem + Img32::BYTES, tid);
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < nkt; kt++) {
+    const bool more = kt + 1 < nkt;
+    if (more) { tk.load(Kp, 64, (kt + 1) * 64, N, tid); tv.load(Vp, 64, (kt + 1) * 64, N, tid); }
+    const char* ks_ = smem + cur * SB;
+    const char* vs_ = ks_ + Img32::BYTES;
+    f32x16 s[2], dp[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; kb++) {
+      s[kb] = mma32(row32(ks_, 32 * kb, 0, lane), qf[0], nl);
+      dp[kb] = mma32(row32(vs_, 32 * kb, 0, lane), of[0], nd);
+#pragma unroll
+      for (int ks = 1; ks < 4; ks++) {
+        s[kb] = mma32(row32(ks_, 32 * kb, ks, lane), qf[ks], s[kb]);
+        dp[kb] = mma32(row32(vs_, 32 * kb, ks, lane), of[ks], dp[kb]);
+      }
+    }
+    // dS^T = exp2(s - lse) * (dp - delta)
+#pragma unroll
+    for (int kb = 0; kb < 2; kb++)
+#pragma unroll
+      for (int i = 0; i < 16; i++) dp[kb][i] *= fexp2(s[kb][i]);
+    if (kt * 64 + 64 > N) {   // last tile: zero dS of keys >= N (exp2(-lse) may overflow)
+#pragma unroll
+      for (int kb = 0; kb < 2; kb++)
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+          if (kt * 64 + 32 * kb + acc_row(i, h) >= N) dp[kb][i] = 0.f;
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; kb++)
+#pragma unroll
+      for (int st = 0; st < 2; st++) {
+        const bf16x8 da = pack_acc(dp[kb], st);
+#pragma unroll
+        for (int db = 0; db < 2; db++) dq[db] = mma32(da, tr32(ks_, 32 * kb + 16 * st, 32 * db, lane), dq[db]);
+      }
+    if (more) { tk.store(smem + (cur ^ 1) * SB, tid); tv.store(smem + (cur ^ 1) * SB + Img32::BYTES, tid); }
+    __syncthreads();
+    cur ^= 1;
+  }
+  if (sink.dqkv) {
+    float csq[2] = {0.f, 0.f};
+    qkv_sink32<bf16>(sink, 0, b, hh, H, q0, N, lane, dq, 0.125f, csq);
+    if (sink.ws) qkv_colsum32(sink, 0, hh, H, (blockIdx.y * gridDim.x + blockIdx.x) % S3OD_NREP, lane, csq);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const int q = q0 + acc_row(i, h);
+    if (q >= N) continue;
+    bf16* r = dQ + ((long)bh * N + q) * 64;
+#pragma unroll
+    for (int db = 0; db < 2; db++) r[32 * db + (lane & 31)] = (bf16)dq[db][i];
+  }
+}
+
 extern "C" {
 
 // q,k,v: [B*H, N, 64] (q pre-scaled by log2(e)/8); o: [B, N, H*64]; lse: [B*H, N] fp32, log2 units (optional)
@@ -773,6 +1088,12 @@ int s3od_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* 
 }  // extern "C"
 
 namespace {
+// bf16 backward body: 1 = 32x32x16 kernels (default), 0 = the 16x16x32 kernels (S3OD_ATTN_BWD=16 selects them,
+// for A/B measurement)
+int attn_bwd_variant() {
+  static int v = [] { const char* e = getenv("S3OD_ATTN_BWD"); return (e && e[0] == '1' && e[1] == '6') ? 0 : 1; }();
+  return v;
+}
 __global__ void qkv_fold_kernel(const float* __restrict__ ws, float* __restrict__ a, float* __restrict__ b, int D) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 2 * D) return;
@@ -788,6 +1109,16 @@ void launch_bwd(const void* q, const void* k, const void* v, const void* o, cons
   // 32 keys (dK/dV pass) / 32 queries (dQ pass) per wave: 64 per wave halves the LDS bytes per MFMA but
   // needs > 256 registers -> one wave per SIMD: the whole backward measured 19 % (dK/dV) / 11 % (dQ) slower at N=4101
   hipLaunchKernelGGL(attn_delta_kernel<T>, dim3(cdiv((long)B * H * N * 8, 256)), dim3(256), 0, st, (const T*)o, (const T*)dout, delta, N, H, B * H);
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (attn_bwd_variant() == 1) {
+      constexpr int W = 4;
+      hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<W>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st, (const bf16*)q, (const bf16*)k,
+                         (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv, N, H, sink);
+      hipLaunchKernelGGL((attn_bwd_dq32_kernel<W>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st, (const bf16*)q, (const bf16*)k,
+                         (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, N, H, sink);
+      return;
+    }
+  }
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, 2>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v,
                      (const T*)dout, lse, delta, (T*)dk, (T*)dv, N, H, sink);
   hipLaunchKernelGGL((attn_bwd_dq_kernel<T, 2>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v,

@@ -97,18 +97,24 @@ class AugParams(ctypes.Structure):
                 ("new_w", ctypes.c_int), ("pad_h", ctypes.c_int), ("pad_w", ctypes.c_int), ("bright", ctypes.c_float),
                 ("contrast", ctypes.c_float), ("sat", ctypes.c_float), ("hue", ctypes.c_float),
                 ("gray_mean", ctypes.c_float), ("mult", ctypes.c_float * 3), ("gauss_std", ctypes.c_float),
-                ("seed", ctypes.c_uint), ("persp", ctypes.c_float * 2), ("kdist", ctypes.c_float), ("raw", ctypes.c_int)]
+                ("seed", ctypes.c_uint), ("persp", ctypes.c_float * 2), ("kdist", ctypes.c_float), ("raw", ctypes.c_int),
+                ("grid", ctypes.c_void_p), ("elastic", ctypes.c_void_p)]
 
 
 class SynthParams(ctypes.Structure):
-    """Mirror of struct SynthParams (csrc/data_ops.hip): the synthetic-mode photometric chain."""
+    """Mirror of struct SynthParams (csrc/data_ops.hip): the photometric chain after the geometry pass."""
     _fields_ = [("bright", ctypes.c_float), ("contrast", ctypes.c_float), ("sat", ctypes.c_float), ("hue", ctypes.c_float),
                 ("gray_mean", ctypes.c_float), ("hsv_h", ctypes.c_float), ("hsv_s", ctypes.c_float), ("hsv_v", ctypes.c_float),
-                ("iso_int", ctypes.c_float), ("iso_color", ctypes.c_float), ("gauss_std", ctypes.c_float),
-                ("mult", ctypes.c_float * 3), ("rbc_alpha", ctypes.c_float), ("rbc_beta", ctypes.c_float),
-                ("n_shadow", ctypes.c_int), ("shadow", (ctypes.c_float * 6) * 3), ("shadow_dim", ctypes.c_float),
-                ("down", ctypes.c_float), ("ksize", ctypes.c_int), ("color_op", ctypes.c_int), ("perm", ctypes.c_int * 3),
-                ("post_bits", ctypes.c_int), ("seed", ctypes.c_uint)]
+                ("clahe_clip", ctypes.c_float), ("iso_intensity", ctypes.c_float), ("iso_color_shift", ctypes.c_float),
+                ("gauss_std", ctypes.c_float), ("mult", ctypes.c_float * 3), ("jpeg_quality", ctypes.c_int),
+                ("down", ctypes.c_float), ("rbc_alpha", ctypes.c_float), ("rbc_beta", ctypes.c_float),
+                ("n_shadow", ctypes.c_int), ("shadow", (ctypes.c_float * 10) * 3), ("shadow_dim", ctypes.c_float),
+                ("ksize", ctypes.c_int), ("zoom_n", ctypes.c_int), ("zoom", ctypes.c_float * 4),
+                ("color_op", ctypes.c_int), ("perm", ctypes.c_int * 3), ("post_bits", ctypes.c_int),
+                ("snow_point", ctypes.c_float), ("snow_coeff", ctypes.c_float),
+                ("rain_n", ctypes.c_int), ("rain_slant", ctypes.c_int), ("rain_len", ctypes.c_int), ("rain_blur", ctypes.c_int),
+                ("rain_color", ctypes.c_float), ("rain_bright", ctypes.c_float), ("order", ctypes.c_int),
+                ("seed", ctypes.c_uint), ("rain_drops", ctypes.c_void_p), ("ws", ctypes.c_void_p)]
 
     @classmethod
     def identity(cls):
@@ -118,6 +124,60 @@ class SynthParams(ctypes.Structure):
         p.rbc_alpha, p.shadow_dim, p.down, p.ksize, p.post_bits = 1.0, 1.0, 1.0, 1, 8
         p.perm[0], p.perm[1], p.perm[2] = 0, 1, 2
         return p
+
+
+class ElasticParams(ctypes.Structure):
+    """Mirror of struct ElasticParams (csrc/data_ops.hip)."""
+    _fields_ = [("w", ctypes.c_float * 33), ("ksize", ctypes.c_int), ("alpha", ctypes.c_float), ("seed", ctypes.c_uint)]
+
+
+def augment_ws_floats(S: int) -> int:
+    """Size (floats) of SynthParams.ws for canvas size S (s3od_augment_ws_floats)."""
+    n = ctypes.c_long(0)
+    lib()("s3od_augment_ws_floats", int(S), ctypes.addressof(n))
+    return int(n.value)
+
+
+def gaussian_taps(ksize: int, sigma: float) -> np.ndarray:
+    """cv2.getGaussianKernel(ksize, sigma) (sigma > 0)."""
+    x = np.arange(ksize) - (ksize - 1) / 2
+    g = np.exp(-x ** 2 / (2 * sigma ** 2))
+    return g / g.sum()
+
+
+def elastic_params(seed: int, alpha: float = 1.0, sigma: float = 25.0, ksize: int = 17) -> ElasticParams:
+    """ElasticTransform(alpha=1, sigma=25) displacement parameters (transforms.py:169-173; albumentations
+    2.0.8 generate_displacement_fields with approximate=False, i.e. a 17x17 Gaussian)."""
+    e = ElasticParams()
+    for i, v in enumerate(gaussian_taps(ksize, sigma)):
+        e.w[i] = float(v)
+    e.ksize, e.alpha, e.seed = ksize, float(alpha), seed & 0xFFFFFFFF
+    return e
+
+
+def grid_distortion_maps(S: int, steps_x, steps_y, num_steps: int = 6):
+    """GridDistortion(num_steps=6, distort_limit=0.3, normalized=True) (transforms.py:164-168): the
+    albumentations 2.0.8 step normalisation (last step scaled to its true width, steps rescaled so the
+    distorted grid ends at the image border) and the separable per-column / per-row source maps
+    (index coordinates) that cv2.remap reads."""
+    def one(size, steps):
+        step = size // num_steps
+        steps = np.asarray(steps, np.float64).copy()
+        last = min(size, (num_steps + 1) * step) - num_steps * step
+        steps[-1] *= last / step
+        steps *= (size / math.floor(size / num_steps)) / steps.sum()
+        m = np.zeros(size, np.float32)
+        prev = 0.0
+        for idx, st in enumerate(steps):
+            start = idx * step
+            end = min(start + step, size)
+            if start >= size:
+                break
+            cur = prev + step * st
+            m[start:end] = np.linspace(prev, cur, end - start, dtype=np.float64).astype(np.float32)
+            prev = cur
+        return m
+    return one(S, steps_x), one(S, steps_y)
 
 
 def _one_of(r, p, weights):
@@ -211,19 +271,36 @@ class GpuAugment:
         rank = torch.distributed.get_rank() if torch.distributed.is_available() and torch.distributed.is_initialized() else 0
         base = torch.initial_seed() if seed is None else int(seed)
         self.rng = random.Random(base * 1000003 + rank)
+        self._ws = None            # SynthParams.ws (CLAHE / ISONoise / JPEG / rain / regular chain)
+        self._elastic = None       # ElasticTransform displacement [2][S][S] + its scratch
 
+    # ------------------------------------------------------------------ draws
     def sample_params(self, h0: int, w0: int, img: Optional[np.ndarray] = None) -> AugParams:
+        """Geometry (+ the regular mode's one-pass photometrics) of one sample."""
+        return self._draw(h0, w0, img)[0]
+
+    def _draw(self, h0, w0, img=None):
+        """-> (AugParams, extra) where extra holds the host-side pieces of the sample's chain: the regular
+        chain's SynthParams + Sharpen kernel when it drew Sharpen or ISONoise, and the GridDistortion maps /
+        ElasticTransform seed of the synthetic distortion group."""
         S, r = self.S, self.rng
         nh, nw, ph, pw = letterbox(h0, w0, S)
         M = np.eye(3)                              # forward map canvas -> output (pixel-centre coords)
         bright = contrast = sat = 1.0
         hue, mult, gstd = 0.0, [1.0, 1.0, 1.0], 0.0
         kdist = 0.0
+        extra = {}
         if self.mode == "synthetic":
             M = self._geometry(M)
-            g = _one_of(r, 0.4, [0.3, 0.3, 0.2, 0.15])           # Optical | Grid* | Elastic* | Perspective
+            g = _one_of(r, 0.4, [0.3, 0.3, 0.2, 0.15])           # Optical | Grid | Elastic | Perspective
             if g == 0:
                 kdist = r.uniform(-0.3, 0.3) * 0.25                 # distort_limit 0.3 on the normalised radius
+            elif g == 1:                                        # GridDistortion(num_steps 6, distort_limit 0.3)
+                sx = [1 + r.uniform(-0.3, 0.3) for _ in range(7)]
+                sy = [1 + r.uniform(-0.3, 0.3) for _ in range(7)]
+                extra["grid"] = grid_distortion_maps(S, sx, sy, 6)
+            elif g == 2:                                        # ElasticTransform(alpha 1, sigma 25)
+                extra["elastic"] = r.getrandbits(32)
             elif g == 3:                                        # Perspective(scale 0.05-0.1): corner jitter
                 sc = r.uniform(0.05, 0.1)
                 src = np.array([[0, 0], [S, 0], [S, S], [0, S]], np.float64)
@@ -238,35 +315,56 @@ class GpuAugment:
                 self._fill(p, h0, w0, nh, nw, ph, pw)
                 p.persp[0], p.persp[1] = float(Tot[2, 0]), float(Tot[2, 1])
                 p.raw = 1
-                return p
+                return p, extra
         elif self.mode != "test":
             M = self._geometry(M)
-            if r.random() < 0.5 and r.random() < 0.7:  # OneOf(ColorJitter p.7, Sharpen p.3) p.5
+            q = None
+            g = _one_of(r, 0.5, [0.7, 0.3])                     # OneOf(ColorJitter p.7, Sharpen p.3) p.5
+            if g == 0:
                 bright, contrast = r.uniform(0.5, 1.5), r.uniform(0.5, 1.5)
                 sat, hue = r.uniform(0.8, 1.2), r.uniform(-0.2, 0.2)
-            if r.random() < 0.3:                      # OneOf(GaussNoise, ISONoise, MultiplicativeNoise) p.3
-                if r.random() < 0.5:
-                    gstd = r.uniform(0.2, 0.44)
-                else:
-                    mult = [r.uniform(0.9, 1.1) for _ in range(3)]
+            elif g == 1:                                        # Sharpen(alpha 0.2-0.5, lightness 0.5-1.0)
+                q = SynthParams.identity()
+                extra["kernel"] = _sharpen_kernel(r.uniform(0.2, 0.5), r.uniform(0.5, 1.0))
+            n = _one_of(r, 0.3, [0.5, 0.5, 0.5])                # OneOf(GaussNoise, ISONoise, MultiplicativeNoise) p.3
+            if n == 0:
+                gstd = r.uniform(0.2, 0.44)
+            elif n == 1:                                        # ISONoise defaults: color_shift 0.01-0.05, intensity 0.1-0.5
+                q = q or SynthParams.identity()
+                q.iso_color_shift, q.iso_intensity = r.uniform(0.01, 0.05), r.uniform(0.1, 0.5)
+            elif n == 2:                                        # MultiplicativeNoise(0.9-1.1), per_channel=False
+                mult = [r.uniform(0.9, 1.1)] * 3
+            if q is not None:                                   # Sharpen / ISONoise: the two-stage regular chain
+                q.order = 1
+                q.bright, q.contrast, q.sat, q.hue = bright, contrast, sat, hue
+                q.gauss_std = gstd
+                for i in range(3):
+                    q.mult[i] = mult[i]
+                if "kernel" in extra:
+                    q.ksize = 3
+                extra["chain"] = q
         Minv = np.linalg.inv(M)
         p = AugParams()
         for i, v in enumerate(list(Minv[0]) + list(Minv[1])):
             p.A[i] = float(v)
         self._fill(p, h0, w0, nh, nw, ph, pw)
         p.kdist = kdist
-        p.raw = int(self.mode == "synthetic")
+        p.raw = int(self.mode == "synthetic" or "chain" in extra)
         p.bright, p.contrast, p.sat, p.hue = bright, contrast, sat, hue
         gm = 0.0
         if contrast != 1.0 and img is not None:       # mean grey of the padded canvas after brightness
-            g = (img[..., 0] * 0.299 + img[..., 1] * 0.587 + img[..., 2] * 0.114).mean() / 255.0
-            gm = min(1.0, g * bright) * (nh * nw) / (S * S)
+            gm = (img[..., 0] * 0.299 + img[..., 1] * 0.587 + img[..., 2] * 0.114).mean() / 255.0
+            gm = min(1.0, gm * bright) * (nh * nw) / (S * S)
         p.gray_mean = gm
+        if "chain" in extra:
+            extra["chain"].gray_mean = gm
         for i in range(3):
             p.mult[i] = mult[i]
         p.gauss_std = gstd
         p.seed = r.getrandbits(32)
-        return p
+        if "chain" in extra:
+            extra["chain"].seed = p.seed
+        return p, extra
 
     @staticmethod
     def _fill(p, h0, w0, nh, nw, ph, pw):
@@ -304,44 +402,53 @@ class GpuAugment:
         return M
 
     def synth_params(self, img: Optional[np.ndarray] = None):
-        """The synthetic-mode photometric groups (transforms.py:65-216): SynthParams + the composed filter."""
+        """The synthetic-mode photometric groups (transforms.py:65-216, albumentations 2.0.8 defaults for the
+        arguments the reference leaves unset): SynthParams + the composed filter taps + the rain drops."""
         S, r = self.S, self.rng
         q = SynthParams.identity()
-        g = _one_of(r, 0.7, [0.7, 0.4, 0.2])                  # ColorJitter | HueSaturationValue | CLAHE*
+        g = _one_of(r, 0.7, [0.7, 0.4, 0.2])                  # ColorJitter | HueSaturationValue | CLAHE
         if g == 0:
             q.bright, q.contrast = r.uniform(0.6, 1.4), r.uniform(0.6, 1.4)
             q.sat, q.hue = r.uniform(0.7, 1.3), r.uniform(-0.2, 0.2)
             if img is not None:
                 gm = (img[..., 0] * 0.299 + img[..., 1] * 0.587 + img[..., 2] * 0.114).mean() / 255.0
                 q.gray_mean = min(1.0, gm * q.bright)
-        elif g == 1:
-            q.hsv_h, q.hsv_s, q.hsv_v = r.uniform(-25, 25), r.uniform(-35, 35) / 255.0, r.uniform(-30, 30) / 255.0
+        elif g == 1:                                          # uint8 HSV: hue in cv2 units of 2 degrees
+            q.hsv_h, q.hsv_s, q.hsv_v = 2.0 * r.uniform(-25, 25), r.uniform(-35, 35) / 255.0, r.uniform(-30, 30) / 255.0
+        elif g == 2:                                          # CLAHE(clip_limit 4.0 -> U(1, 4), 8x8 tiles)
+            q.clahe_clip = r.uniform(1.0, 4.0)
         g = _one_of(r, 0.6, [0.4, 0.4, 0.4])                  # ISONoise | GaussNoise | MultiplicativeNoise
         if g == 0:
-            q.iso_color, q.iso_int = r.uniform(0.01, 0.03), r.uniform(0.08, 0.3) * 0.2
+            q.iso_color_shift, q.iso_intensity = r.uniform(0.01, 0.03), r.uniform(0.08, 0.3)
         elif g == 1:
             q.gauss_std = r.uniform(0.25, 0.6)
         elif g == 2:
-            for i in range(3):
-                q.mult[i] = r.uniform(0.9, 1.1)
-        g = _one_of(r, 0.5, [0.4, 0.3])                       # ImageCompression* | Downscale
-        if g == 1:
+            q.mult[0] = q.mult[1] = q.mult[2] = r.uniform(0.9, 1.1)
+        g = _one_of(r, 0.5, [0.4, 0.3])                       # ImageCompression | Downscale
+        if g == 0:
+            q.jpeg_quality = r.randint(30, 80)
+        elif g == 1:
             q.down = r.uniform(0.4, 0.7)
         g = _one_of(r, 0.5, [0.4, 0.4])                       # RandomShadow | RandomBrightnessContrast
-        if g == 0:
+        if g == 0:                                            # 1-3 pentagons in shadow_roi (0, 0.1, 1, 1)
             q.n_shadow, q.shadow_dim = r.randint(1, 3), 0.5
-            for t in range(q.n_shadow):                         # shadow_roi (0, 0.1, 1, 1)
-                for v in range(3):
-                    q.shadow[t][2 * v], q.shadow[t][2 * v + 1] = r.uniform(0, S), r.uniform(0.1 * S, S)
+            for t in range(q.n_shadow):
+                for v in range(5):
+                    q.shadow[t][2 * v], q.shadow[t][2 * v + 1] = r.randrange(0, S), r.randrange(int(0.1 * S), S)
         elif g == 1:
             q.rbc_alpha, q.rbc_beta = 1.0 + r.uniform(-0.4, 0.4), r.uniform(-0.4, 0.4)
         ker = np.ones((1, 1))
-        g = _one_of(r, 0.5, [0.4, 0.4, 0.3, 0.2])             # MotionBlur | GaussianBlur | Defocus | ZoomBlur*
+        g = _one_of(r, 0.5, [0.4, 0.4, 0.3, 0.2])             # MotionBlur | GaussianBlur | Defocus | ZoomBlur
         if g in (0, 1):
             k = r.choice([3, 5, 7])
             ker = _motion_kernel(r, k) if g == 0 else _gauss_kernel(k)
         elif g == 2:
             ker = _disk_kernel(r.randint(2, 6), r.uniform(0.1, 0.3))
+        elif g == 3:                                          # ZoomBlur(max_factor 1.03, step_factor 0.01-0.03)
+            z = np.arange(1.0, r.uniform(1.0, 1.03), r.uniform(0.01, 0.03))[:4]
+            q.zoom_n = len(z)
+            for i, v in enumerate(z):
+                q.zoom[i] = float(v)
         g = _one_of(r, 0.05, [0.5, 0.5, 0.3])                 # ToSepia | ToGray | ChannelShuffle
         if g is not None:
             q.color_op = g + 1
@@ -355,11 +462,48 @@ class GpuAugment:
             ker = _conv_full(ker, _sharpen_kernel(r.uniform(0.2, 0.6), r.uniform(0.5, 1.2)))
         elif g == 2:
             q.post_bits = 5
-        _one_of(r, 0.15, [0.1, 0.1])                           # RandomSnow* | RandomRain*
+        drops = None
+        g = _one_of(r, 0.15, [0.1, 0.1])                      # RandomSnow | RandomRain
+        if g == 0:                                            # bleach, snow_point 0.1-0.3, brightness_coeff 2.5
+            q.snow_point, q.snow_coeff = r.uniform(0.1, 0.3), 2.5
+        elif g == 1:                                          # default rain: S*S // 600 drops of length 20
+            slant = int(r.uniform(-10, 10))
+            n = S * S // 600
+            lo, hi = (-slant, S) if slant < 0 else (0, S - slant)
+            drops = np.array([[r.randrange(lo, hi), r.randrange(0, S - 20)] for _ in range(n)], np.int32)
+            q.rain_n, q.rain_slant, q.rain_len, q.rain_blur = n, slant, 20, 7
+            q.rain_color, q.rain_bright = 200.0 / 255.0, 0.7
         q.ksize = ker.shape[0]
         q.seed = r.getrandbits(32)
         kw = torch.tensor(ker.reshape(-1), dtype=torch.float32).to(self.device, non_blocking=True) if q.ksize > 1 else None
-        return q, kw
+        dr = torch.from_numpy(drops).to(self.device, non_blocking=True) if drops is not None else None
+        if dr is not None:
+            q.rain_drops = dr.data_ptr()
+        return q, kw, dr
+
+    # ------------------------------------------------------------------ device buffers
+    def workspace(self):
+        if self._ws is None:
+            self._ws = torch.empty(augment_ws_floats(self.S), dtype=torch.float32, device=self.device)
+        return self._ws
+
+    def _elastic_field(self, seed):
+        S = self.S
+        if self._elastic is None:
+            self._elastic = torch.empty((2, 2, S, S), dtype=torch.float32, device=self.device)
+        e = elastic_params(seed)
+        lib()("s3od_elastic_field", ctypes.addressof(e), S, self._elastic[1], self._elastic[0], stream())
+        return self._elastic[0]
+
+    def _attach(self, p, extra, keep):
+        """Device tables of the distortion group -> AugParams pointers."""
+        if "grid" in extra:
+            gx, gy = extra["grid"]
+            g = torch.from_numpy(np.concatenate([gx, gy]).astype(np.float32)).to(self.device, non_blocking=True)
+            p.grid = g.data_ptr()
+            keep.append(g)
+        if "elastic" in extra:
+            p.elastic = self._elastic_field(extra["elastic"]).data_ptr()
 
     def __call__(self, samples: List[Dict[str, np.ndarray]]) -> Dict[str, torch.Tensor]:
         B, S, dev = len(samples), self.S, self.device
@@ -370,11 +514,22 @@ class GpuAugment:
             img = torch.from_numpy(np.ascontiguousarray(smp["image"], dtype=np.uint8)).pin_memory().to(dev, non_blocking=True)
             msk = torch.from_numpy(np.ascontiguousarray(smp["mask"], dtype=np.uint8)).pin_memory().to(dev, non_blocking=True)
             h0, w0 = smp["image"].shape[:2]
-            prm = self.sample_params(h0, w0, smp["image"])
+            prm, extra = self._draw(h0, w0, smp["image"])
+            self._attach(prm, extra, keep)
             if self.mode == "synthetic":
                 raw = torch.empty((3, S, S), dtype=torch.float32, device=dev)
                 lib()("s3od_augment_sample", img, msk, ctypes.addressof(prm), S, raw, masks[b], stream())
-                q, kw = self.synth_params(smp["image"])
+                q, kw, dr = self.synth_params(smp["image"])
+                q.ws = self.workspace().data_ptr()
+                lib()("s3od_augment_synthetic", raw, ctypes.addressof(q), kw, S, images[b], stream())
+                keep.append((img, msk, raw, kw, dr))
+                continue
+            if "chain" in extra:                       # regular mode drew Sharpen and / or ISONoise
+                raw = torch.empty((3, S, S), dtype=torch.float32, device=dev)
+                lib()("s3od_augment_sample", img, msk, ctypes.addressof(prm), S, raw, masks[b], stream())
+                q = extra["chain"]
+                q.ws = self.workspace().data_ptr()
+                kw = torch.tensor(extra["kernel"].reshape(-1), dtype=torch.float32).to(dev) if "kernel" in extra else None
                 lib()("s3od_augment_synthetic", raw, ctypes.addressof(q), kw, S, images[b], stream())
                 keep.append((img, msk, raw, kw))
                 continue

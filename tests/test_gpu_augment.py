@@ -1,0 +1,273 @@
+"""GPU: the training-augmentation members built on device (§8(f)3; synth_sod/.../transforms.py:12-224)
+against oracle/augment_oracle.py, the numpy restatement of albumentations 2.0.8 / OpenCV 4.12's published
+algorithms (neither library is installed: parity with them is unpinned; these tests pin the kernels to
+the restated algorithms).  Each member runs alone through the C ABI on a seeded [0,1] image:
+
+* CLAHE (8x8 tiles, clip 2.5) and ISONoise: the 8-bit L / Poisson draws can flip on float32-vs-float64
+  rounding, so <= 0.2 % of pixels may differ by more than 1e-3 (CLAHE: float32 Lab round trip) / 1e-4;
+* ImageCompression at quality 30 / 75 and a canvas that is not a multiple of the 16-pixel MCU: <= 0.5 %
+  of pixels more than one 8-bit step away, mean |d| <= 2e-3;
+* ZoomBlur (+ Sharpen composed), Downscale + RandomBrightnessContrast, RandomShadow, RandomSnow,
+  RandomRain, GridDistortion, ElasticTransform: <= 1e-4 (shadow / snow: <= 0.1 % of pixels on a
+  polygon edge / threshold may differ);
+* the regular chain's Sharpen -> ISONoise order."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import augment_oracle as AO
+
+pytestmark = pytest.mark.gpu
+MEAN = np.array([0.485, 0.456, 0.406])[:, None, None]
+STD = np.array([0.229, 0.224, 0.225])[:, None, None]
+
+
+def _img(S, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.rand(3, S // 4, S // 4, device="cuda", generator=g)[None]
+    x = torch.nn.functional.interpolate(x, size=(S, S), mode="bilinear", align_corners=False)[0]
+    return (x + 0.15 * torch.rand(3, S, S, device="cuda", generator=g)).clamp(0, 1).contiguous()
+
+
+def _run(raw, q, kw=None, ws=True):
+    from s3od_amd._lib import lib, stream
+    from s3od_amd.data import augment_ws_floats
+    S = raw.shape[-1]
+    keep = None
+    if ws:
+        keep = torch.empty(augment_ws_floats(S), device="cuda")
+        q.ws = keep.data_ptr()
+    out = torch.empty(3, S, S, device="cuda")
+    src = raw.clone()
+    lib()("s3od_augment_synthetic", src, ctypes.addressof(q), kw, S, out, stream())
+    torch.cuda.synchronize()
+    return out.cpu().numpy().astype(np.float64) * STD + MEAN
+
+
+def _frac(a, b, tol):
+    return float((np.abs(a - b) > tol).mean())
+
+
+@pytest.mark.parametrize("S", [64, 96])
+def test_clahe(S):
+    from s3od_amd.data import SynthParams
+    x = _img(S, 1)
+    q = SynthParams.identity()
+    q.clahe_clip = 2.5
+    got = _run(x, q)
+    ref = AO.clahe(x.cpu().numpy().astype(np.float64), 2.5)
+    # float32 Lab round trip on device (~1e-4 near black) vs float64 here; flipped 8-bit L values
+    assert _frac(got, ref, 1e-3) <= 2e-3 and np.abs(got - ref).max() < 0.05, (_frac(got, ref, 1e-3), np.abs(got - ref).max())
+    assert np.abs(got - x.cpu().numpy()).mean() > 1e-3          # the member did something
+
+
+def test_iso_noise():
+    from s3od_amd.data import SynthParams
+    S = 96
+    x = _img(S, 2)
+    q = SynthParams.identity()
+    q.iso_intensity, q.iso_color_shift, q.seed = 0.3, 0.03, 1234
+    got = _run(x, q)
+    ref = AO.iso_noise(x.cpu().numpy().astype(np.float64), 0.3, 0.03, 1234)
+    f = _frac(got, ref, 1e-4)
+    assert f <= 2e-3, f
+    assert np.abs(got - x.cpu().numpy()).mean() > 1e-3
+
+
+@pytest.mark.parametrize("S,quality", [(64, 30), (72, 75), (96, 55)])
+def test_jpeg(S, quality):
+    from s3od_amd.data import SynthParams
+    x = _img(S, 3)
+    q = SynthParams.identity()
+    q.jpeg_quality = quality
+    got = _run(x, q)
+    ref = AO.jpeg(x.cpu().numpy().astype(np.float64), quality)
+    f = _frac(got, ref, 1.5 / 255)
+    assert f <= 5e-3 and np.abs(got - ref).mean() <= 2e-3, (f, np.abs(got - ref).mean())
+    assert np.abs(got - x.cpu().numpy()).mean() > 1e-3
+
+
+@pytest.mark.parametrize("with_sharpen", [False, True])
+def test_zoom_blur(with_sharpen):
+    from s3od_amd.data import SynthParams, _sharpen_kernel
+    S = 96
+    x = _img(S, 4)
+    q = SynthParams.identity()
+    zs = [1.0, 1.01, 1.02]
+    q.zoom_n = 3
+    for i, z in enumerate(zs):
+        q.zoom[i] = z
+    kw, ker = None, None
+    if with_sharpen:
+        ker = _sharpen_kernel(0.4, 0.8)
+        q.ksize = 3
+        kw = torch.tensor(ker.reshape(-1), dtype=torch.float32, device="cuda")
+    got = _run(x, q, kw, ws=False)
+    v = AO.zoom_blur(x.cpu().numpy().astype(np.float64), np.float32(zs))
+    ref = AO.filter2d(v, ker) if with_sharpen else np.clip(v, 0, 1)
+    assert np.abs(got - ref).max() <= 1e-4
+
+
+def test_downscale_brightness_contrast():
+    from s3od_amd.data import SynthParams
+    S = 96
+    x = _img(S, 5)
+    q = SynthParams.identity()
+    q.down, q.rbc_alpha, q.rbc_beta = 0.55, 1.3, -0.1
+    got = _run(x, q, ws=False)
+    ref = AO.lit(x.cpu().numpy().astype(np.float64), down=0.55, rbc=(1.3, -0.1))
+    assert np.abs(got - ref).max() <= 1e-4
+
+
+def test_random_shadow_pentagons():
+    from s3od_amd.data import SynthParams
+    S = 96
+    x = _img(S, 6)
+    r = np.random.default_rng(0)
+    q = SynthParams.identity()
+    polys = [r.integers(0, S, 10).astype(float) for _ in range(3)]
+    q.n_shadow, q.shadow_dim = 3, 0.5
+    for t, pv in enumerate(polys):
+        for i, v in enumerate(pv):
+            q.shadow[t][i] = float(v)
+    got = _run(x, q, ws=False)
+    ref = AO.lit(x.cpu().numpy().astype(np.float64), shadows=polys, shadow_dim=0.5)
+    assert _frac(got, ref, 1e-4) <= 1e-3
+    assert np.abs(got - x.cpu().numpy()).max() > 0.05
+
+
+def test_snow_bleach():
+    from s3od_amd.data import SynthParams
+    S = 64
+    x = _img(S, 7)
+    q = SynthParams.identity()
+    q.snow_point, q.snow_coeff = 0.2, 2.5
+    got = _run(x, q, ws=False)
+    ref = AO.snow_bleach(x.cpu().numpy().astype(np.float64), 0.2, 2.5)
+    assert _frac(got, ref, 1e-4) <= 1e-3
+
+
+@pytest.mark.parametrize("slant", [-7, 0, 9])
+def test_rain(slant):
+    from s3od_amd.data import SynthParams
+    S = 96
+    x = _img(S, 8)
+    r = np.random.default_rng(slant + 20)
+    n = S * S // 600
+    lo, hi = (-slant, S) if slant < 0 else (0, S - slant)
+    drops = np.stack([r.integers(lo, hi, n), r.integers(0, S - 20, n)], 1).astype(np.int32)
+    dr = torch.from_numpy(drops).cuda()
+    q = SynthParams.identity()
+    q.rain_n, q.rain_slant, q.rain_len, q.rain_blur, q.rain_color, q.rain_bright = n, slant, 20, 7, 200 / 255, 0.7
+    q.rain_drops = dr.data_ptr()
+    got = _run(x, q)
+    ref = AO.rain(x.cpu().numpy().astype(np.float64), drops, slant)
+    assert np.abs(got - ref).max() <= 1e-4
+
+
+def _geometry(S, p_mod):
+    """test-mode letterbox of a seeded uint8 image, then the distortion member through the geometry pass
+    (raw [0,1] output) vs cv2.remap of the undistorted canvas."""
+    from s3od_amd._lib import lib, stream
+    from s3od_amd.data import GpuAugment
+    r = np.random.default_rng(3)
+    img = r.integers(0, 256, (S - 10, S, 3), dtype=np.uint8)
+    msk = (r.random((S - 10, S)) > 0.5).astype(np.uint8) * 255
+    aug = GpuAugment(S, mode="test")
+    p = aug.sample_params(S - 10, S)
+    p.raw = 1
+    ti, tm = torch.from_numpy(img).cuda(), torch.from_numpy(msk).cuda()
+    base = torch.empty(3, S, S, device="cuda"); bm = torch.empty(S, S, device="cuda")
+    lib()("s3od_augment_sample", ti, tm, ctypes.addressof(p), S, base, bm, stream())
+    keep = p_mod(p)
+    out = torch.empty(3, S, S, device="cuda"); om = torch.empty(S, S, device="cuda")
+    lib()("s3od_augment_sample", ti, tm, ctypes.addressof(p), S, out, om, stream())
+    torch.cuda.synchronize()
+    del keep
+    return base.cpu().numpy().astype(np.float64), out.cpu().numpy().astype(np.float64), om.cpu().numpy()
+
+
+def test_grid_distortion():
+    from s3od_amd.data import grid_distortion_maps
+    S = 96
+    r = np.random.default_rng(11)
+    gx, gy = grid_distortion_maps(S, 1 + r.uniform(-0.3, 0.3, 7), 1 + r.uniform(-0.3, 0.3, 7), 6)
+    assert abs(float(gx[-1]) - S) < 1e-3 and gx[0] == 0 and np.all(np.diff(gx) >= 0)
+
+    def mod(p):
+        g = torch.from_numpy(np.concatenate([gx, gy]).astype(np.float32)).cuda()
+        p.grid = g.data_ptr()
+        return g
+    base, out, om = _geometry(S, mod)
+    ref = AO.remap_bilinear(base, gx[None, :].astype(np.float64) + 0 * gy[:, None], gy[:, None].astype(np.float64) + 0 * gx[None, :])
+    assert np.abs(out - ref).max() <= 1e-4
+    assert np.abs(out - base).max() > 0.05
+
+
+def test_elastic_transform():
+    from s3od_amd._lib import lib, stream
+    from s3od_amd.data import elastic_params
+    S = 96
+    e = elastic_params(777, alpha=3.0)                 # alpha raised so the warp is visible in the check
+    tmp = torch.empty(2, S, S, device="cuda"); fld = torch.empty(2, S, S, device="cuda")
+    lib()("s3od_elastic_field", ctypes.addressof(e), S, tmp, fld, stream())
+    torch.cuda.synchronize()
+    dx, dy = AO.elastic_field(S, 777, alpha=3.0)
+    f = fld.cpu().numpy()
+    assert np.abs(f[0] - dx).max() <= 1e-5 * max(1.0, np.abs(dx).max()) and np.abs(f[1] - dy).max() <= 1e-5 * max(1.0, np.abs(dy).max())
+
+    def mod(p):
+        p.elastic = fld.data_ptr()
+        return fld
+    base, out, om = _geometry(S, mod)
+    yy, xx = np.mgrid[0:S, 0:S].astype(np.float64)
+    ref = AO.remap_bilinear(base, xx + f[0], yy + f[1])
+    assert np.abs(out - ref).max() <= 1e-4
+
+
+def test_regular_chain_sharpen_then_iso():
+    """transforms.py:44-62 order: Sharpen (colour OneOf) before ISONoise (noise OneOf), then Normalize."""
+    from s3od_amd.data import SynthParams, _sharpen_kernel
+    S = 64
+    x = _img(S, 9)
+    ker = _sharpen_kernel(0.35, 0.7)
+    q = SynthParams.identity()
+    q.order, q.ksize = 1, 3
+    q.iso_intensity, q.iso_color_shift, q.seed = 0.4, 0.04, 99
+    kw = torch.tensor(ker.reshape(-1), dtype=torch.float32, device="cuda")
+    got = _run(x, q, kw)
+    ref = AO.iso_noise(AO.filter2d(x.cpu().numpy().astype(np.float64), ker), 0.4, 0.04, 99)
+    assert _frac(got, ref, 1e-4) <= 2e-3
+
+
+@pytest.mark.parametrize("mode", ["regular", "synthetic"])
+def test_modes_draw_every_member(mode, monkeypatch):
+    """Every member of the mode is reachable through GpuAugment's draws: run enough samples that each
+    OneOf group draws each member, check the outputs are finite, in range and reproducible."""
+    from s3od_amd import data as D
+    seen = set()
+    real_one_of = D._one_of
+
+    def spy(r, p, weights):
+        g = real_one_of(r, p, weights)
+        seen.add((len(weights), tuple(weights), g))
+        return g
+    monkeypatch.setattr(D, "_one_of", spy)
+    r = np.random.default_rng(1)
+    smps = [{"image": r.integers(0, 256, (70 + i % 9, 64, 3), dtype=np.uint8),
+             "mask": (r.random((70 + i % 9, 64)) > 0.5).astype(np.uint8) * 255} for i in range(16)]
+    a = D.GpuAugment(64, mode=mode, seed=3)
+    outs = [a(smps[i:i + 4]) for i in range(0, 16, 4) for _ in range(12)]
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.isfinite(o["images"]).all()
+        lo = torch.tensor(((0 - MEAN) / STD).ravel(), dtype=torch.float32).view(1, 3, 1, 1).cuda()
+        hi = torch.tensor(((1 - MEAN) / STD).ravel(), dtype=torch.float32).view(1, 3, 1, 1).cuda()
+        assert (o["images"] >= lo - 1e-4).all() and (o["images"] <= hi + 1e-4).all()
+    groups = {}
+    for n, w, g in seen:
+        groups.setdefault((n, w), set()).add(g)
+    for (n, w), gs in groups.items():
+        assert set(range(n)) <= gs, (w, gs)

@@ -29,7 +29,7 @@ def timeit(fn, n=10):
 
 def main(out_path):
     res = {}
-    tag = f"KS={os.environ.get('S3OD_ATTN_KS', '2')} QS={os.environ.get('S3OD_ATTN_QS', '2')}"
+    tag = f"bwd={os.environ.get('S3OD_ATTN_BWD', '32')}"
     for B, N in ((16, 4101), (4, 16389)):
         H = 12
         g = torch.Generator(device="cuda").manual_seed(B * N)
@@ -47,7 +47,7 @@ def main(out_path):
         tb = timeit(bwd)
         fl = 4.0 * B * H * N * N * 64
         print(f"{tag} B{B} N{N}: fwd {tf * 1e6:8.1f} us {fl / tf / 1e12:7.1f} TF/s | bwd {tb * 1e6:8.1f} us "
-              f"{2.5 * fl / tb / 1e12:7.1f} TF/s (algorithmic 2.5x fwd)", flush=True)
+              f"{2.0 * fl / tb / 1e12:7.1f} TF/s (algorithmic 2x fwd, SURVEY 8d)", flush=True)
         res[N] = {"o": o.cpu(), "dq": dq.cpu(), "dk": dk.cpu(), "dv": dv.cpu(), "tf": tf, "tb": tb}
     torch.save(res, out_path)
 

@@ -50,6 +50,8 @@ REF = {
     "s3od_sigmoid_unpad_resize": "remove_background post-processing: src/s3od/predictor.py:113-132, src/s3od/utils.py:32-37",
     "s3od_augment_sample": "get_transforms geometry (LongestMaxSize + PadIfNeeded + flip/affine/perspective/optical distortion) + Normalize, one launch per sample: synth_sod/src/synth_sod/model_training/transforms.py:12-64, 205-222",
     "s3od_augment_synthetic": "get_transforms(mode='synthetic') photometric OneOf groups on the geometric result: synth_sod/src/synth_sod/model_training/transforms.py:65-204, 220",
+    "s3od_elastic_field": "ElasticTransform(alpha=1, sigma=25) displacement fields (albumentations 2.0.8 generate_displacement_fields): synth_sod/src/synth_sod/model_training/transforms.py:169-173",
+    "s3od_augment_ws_floats": "workspace size of s3od_augment_synthetic (new; albumentations allocates numpy temporaries)",
     "s3od_eval_metrics": "EvaluationMetrics.step (MAE, MaxF/AvgF, S-measure) + EMeasure + WeightedFMeasure on device: synth_sod/src/synth_sod/model_training/metrics.py:14-424",
     "s3od_eval_metrics_ws": "scratch size of s3od_eval_metrics (new; the reference allocates numpy temporaries)",
     "s3od_preprocess": "BackgroundRemoval._preprocess normalisation: src/s3od/predictor.py:79-94",
