@@ -1094,11 +1094,11 @@ int attn_bwd_variant() {
   static int v = [] { const char* e = getenv("S3OD_ATTN_BWD"); return (e && e[0] == '1' && e[1] == '6') ? 0 : 1; }();
   return v;
 }
-__global__ void qkv_fold_kernel(const float* __restrict__ ws, float* __restrict__ a, float* __restrict__ b, int D) {
+__global__ void qkv_fold_kernel(float* __restrict__ ws, float* __restrict__ a, float* __restrict__ b, int D) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 2 * D) return;
   float s = 0.f;
-  for (int r = 0; r < S3OD_NREP; r++) s += ws[(long)r * 2 * D + i];
+  for (int r = 0; r < S3OD_NREP; r++) { s += ws[(long)r * 2 * D + i]; ws[(long)r * 2 * D + i] = 0.f; }
   if (i < D) { if (a) a[i] += s; }
   else if (b) b[i - D] += s;
 }
@@ -1139,8 +1139,8 @@ int s3od_attn_bwd(int dtype, const void* q, const void* k, const void* v, const 
 
 // backward fused with the QKV+RoPE projection's output gradient: d_qkv [B*N][3*H*64] (T) with the
 // inverse RoPE on the last P tokens (cos_t / sin_t: [P][64] fp32, the forward's tables), q x 1/8,
-// and dbq / dbv (fp32 [H*64], nullable) += column sums; ws: S3OD_NREP * 2 * H*64 floats (nullable
-// when both bias gradients are null).  Replaces s3od_attn_bwd + s3od_qkv_unrope.
+// and dbq / dbv (fp32 [H*64], nullable) += column sums; ws: S3OD_NREP * 2 * H*64 floats, all zero on entry
+// and left all zero (nullable when both bias gradients are null).  Replaces s3od_attn_bwd + s3od_qkv_unrope.
 int s3od_attn_bwd_qkv(int dtype, const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
                       float* delta, const float* cos_t, const float* sin_t, int P, void* dqkv, float* dbq, float* dbv,
                       float* ws, int B, int H, int N, void* stream) {
@@ -1148,7 +1148,6 @@ int s3od_attn_bwd_qkv(int dtype, const void* q, const void* k, const void* v, co
   S3OD_REQUIRE(ws || (!dbq && !dbv), "attn_bwd_qkv: bias gradients need the workspace");
   hipStream_t st = (hipStream_t)stream;
   const int D = 64 * H;
-  if (ws) (void)hipMemsetAsync(ws, 0, sizeof(float) * S3OD_NREP * 2 * D, st);
   QkvSink sink{dqkv, cos_t, sin_t, ws, P};
   DISPATCH_T(dtype, { launch_bwd<T>(q, k, v, o, dout, lse, delta, nullptr, nullptr, nullptr, sink, B, H, N, st); });
   if (ws) hipLaunchKernelGGL(qkv_fold_kernel, dim3(cdiv(2 * D, 256)), dim3(256), 0, st, ws, dbq, dbv, D);

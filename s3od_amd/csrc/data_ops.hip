@@ -447,22 +447,32 @@ __global__ void synth_pixel_kernel(const float* in, float* out, SynthParams P, i
 }
 
 // ---------------------------------------------------------------- ImageCompression (JPEG, 4:2:0)
-struct JpegParams {
-  float dct[8][8];            // dct[u][x] = c(u)/2 cos((2x+1)u pi/16), orthonormal 8-point DCT-II
-  float q[2][64];             // quality-scaled luma / chroma tables (natural order)
-};
+// IJG Annex K base tables (natural order); scaled per quality inside the kernel.  The DCT matrix and the
+// tables are built per workgroup in LDS: a per-lane (divergent) index into a by-value kernel argument
+// miscompiled here (the lanes read one lane's element), so no table rides in the kernel arguments.
+__constant__ int kJpegBase[2][64] = {
+    {16, 11, 10, 16, 24, 40, 51, 61, 12, 12, 14, 19, 26, 58, 60, 55, 14, 13, 16, 24, 40, 57, 69, 56,
+     14, 17, 22, 29, 51, 87, 80, 62, 18, 22, 37, 56, 68, 109, 103, 77, 24, 35, 55, 64, 81, 104, 113, 92,
+     49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99},
+    {17, 18, 24, 47, 99, 99, 99, 99, 18, 21, 26, 66, 99, 99, 99, 99, 24, 26, 56, 99, 99, 99, 99, 99,
+     47, 66, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99,
+     99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99}};
 
 // one 8x8 block per workgroup (64 threads): level-shifted samples -> DCT -> quantise -> dequantise ->
 // IDCT -> rounded 8-bit samples into the Y [Sp][Sp] / Cb, Cr [Sp/2][Sp/2] planes
-__global__ void jpeg_block_kernel(const float* __restrict__ x, int S, JpegParams J, float* __restrict__ yplane,
+__global__ void jpeg_block_kernel(const float* __restrict__ x, int S, int quality, float* __restrict__ yplane,
                                   float* __restrict__ cplane) {
-  __shared__ float f[8][8], t[8][8];
+  __shared__ float f[8][8], t[8][8], dm[8][8];
   const int tid = threadIdx.x, i = tid & 7, j = tid >> 3;
   const int Sp = 16 * ((S + 15) / 16), nby = Sp / 8, nbc = Sp / 16;
   const long plane = (long)S * S;
   int b = blockIdx.x, comp, bx, by;
   if (b < nby * nby) { comp = 0; bx = b % nby; by = b / nby; }
   else { b -= nby * nby; comp = 1 + b / (nbc * nbc); b %= nbc * nbc; bx = b % nbc; by = b / nbc; }
+  // dm[u][k] = c(u)/2 cos((2k+1) u pi / 16): the orthonormal 8-point DCT-II
+  dm[j][i] = (j == 0 ? 0.70710678f : 1.f) * 0.5f * cosf((float)((2 * i + 1) * j) * 0.19634954f);
+  const int q = max(quality, 1), qscale = q < 50 ? 5000 / q : 200 - 2 * q;
+  const float qv = (float)min(max((kJpegBase[comp == 0 ? 0 : 1][j * 8 + i] * qscale + 50) / 100, 1), 255);
   float sample;
   if (comp == 0) {
     const int px = min(bx * 8 + i, S - 1), py = min(by * 8 + j, S - 1);
@@ -483,27 +493,26 @@ __global__ void jpeg_block_kernel(const float* __restrict__ x, int S, JpegParams
   }
   f[j][i] = sample - 128.f;
   __syncthreads();
-  float a = 0.f;                                      // rows: t[y][u] = sum_x dct[u][x] f[y][x]
+  float a = 0.f;                                      // rows: t[y][u] = sum_x dm[u][x] f[y][x]
 #pragma unroll
-  for (int k = 0; k < 8; k++) a += J.dct[i][k] * f[j][k];
+  for (int k = 0; k < 8; k++) a += dm[i][k] * f[j][k];
   t[j][i] = a;
   __syncthreads();
-  a = 0.f;                                            // columns: F[v][u] = sum_y dct[v][y] t[y][u]
+  a = 0.f;                                            // columns: F[v][u] = sum_y dm[v][y] t[y][u]
 #pragma unroll
-  for (int k = 0; k < 8; k++) a += J.dct[j][k] * t[k][i];
-  const float qv = J.q[comp == 0 ? 0 : 1][j * 8 + i];
+  for (int k = 0; k < 8; k++) a += dm[j][k] * t[k][i];
   const float F = rintf(a / qv) * qv;
   __syncthreads();
   f[j][i] = F;
   __syncthreads();
-  a = 0.f;                                            // inverse columns: t[y][u] = sum_v dct[v][y] F[v][u]
+  a = 0.f;                                            // inverse columns: t[y][u] = sum_v dm[v][y] F[v][u]
 #pragma unroll
-  for (int k = 0; k < 8; k++) a += J.dct[k][j] * f[k][i];
+  for (int k = 0; k < 8; k++) a += dm[k][j] * f[k][i];
   t[j][i] = a;
   __syncthreads();
-  a = 0.f;                                            // inverse rows: g[y][x] = sum_u dct[u][x] t[y][u]
+  a = 0.f;                                            // inverse rows: g[y][x] = sum_u dm[u][x] t[y][u]
 #pragma unroll
-  for (int k = 0; k < 8; k++) a += J.dct[k][i] * t[j][k];
+  for (int k = 0; k < 8; k++) a += dm[k][i] * t[j][k];
   const float v = fminf(fmaxf(rintf(a + 128.f), 0.f), 255.f);
   if (comp == 0) yplane[(long)(by * 8 + j) * Sp + bx * 8 + i] = v;
   else cplane[(long)(comp - 1) * (Sp / 2) * (Sp / 2) + (long)(by * 8 + j) * (Sp / 2) + bx * 8 + i] = v;
@@ -695,7 +704,7 @@ int s3od_augment_synthetic(float* raw, const void* params, const float* kw, int 
       src = scratch;
     }
     if (P.iso_intensity > 0.f) {
-      hipMemsetAsync(stats, 0, 2 * sizeof(double), st);
+      (void)hipMemsetAsync(stats, 0, 2 * sizeof(double), st);
       hipLaunchKernelGGL(lightness_stats_kernel, grid, blk, 0, st, src, P, S, stats);
     }
     hipLaunchKernelGGL(synth_pixel_kernel, grid, blk, 0, st, src, out, P, S, (const double*)stats, 1);
@@ -709,31 +718,17 @@ int s3od_augment_synthetic(float* raw, const void* params, const float* kw, int 
     hipLaunchKernelGGL(clahe_apply_kernel, grid, blk, 0, st, raw, S, lut);
   }
   if (P.iso_intensity > 0.f) {
-    hipMemsetAsync(stats, 0, 2 * sizeof(double), st);
+    (void)hipMemsetAsync(stats, 0, 2 * sizeof(double), st);
     hipLaunchKernelGGL(lightness_stats_kernel, grid, blk, 0, st, raw, P, S, stats);
   }
   hipLaunchKernelGGL(synth_pixel_kernel, grid, blk, 0, st, raw, raw, P, S, (const double*)stats, 0);
   if (P.jpeg_quality > 0) {
     // image_compression: cv2.imencode(".jpg", quality) + imdecode (standard tables, 4:2:0)
-    static const int base[2][64] = {
-        {16, 11, 10, 16, 24, 40, 51, 61, 12, 12, 14, 19, 26, 58, 60, 55, 14, 13, 16, 24, 40, 57, 69, 56,
-         14, 17, 22, 29, 51, 87, 80, 62, 18, 22, 37, 56, 68, 109, 103, 77, 24, 35, 55, 64, 81, 104, 113, 92,
-         49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99},
-        {17, 18, 24, 47, 99, 99, 99, 99, 18, 21, 26, 66, 99, 99, 99, 99, 24, 26, 56, 99, 99, 99, 99, 99,
-         47, 66, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99,
-         99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99}};
-    JpegParams J;
-    const int q = max(P.jpeg_quality, 1), scale = q < 50 ? 5000 / q : 200 - 2 * q;
-    for (int t = 0; t < 2; t++)
-      for (int i = 0; i < 64; i++) J.q[t][i] = (float)std::min(std::max((base[t][i] * scale + 50) / 100, 1), 255);
-    for (int u = 0; u < 8; u++)
-      for (int k = 0; k < 8; k++)
-        J.dct[u][k] = (float)((u == 0 ? 0.7071067811865476 : 1.0) * 0.5 * cos((2 * k + 1) * u * 3.141592653589793 / 16.0));
     const int Sp = (int)ws_sp(S);
     float* yp = ws + ws_jpeg_y(S);
     float* cp = ws + ws_jpeg_c(S);
     const int nblk = (Sp / 8) * (Sp / 8) + 2 * (Sp / 16) * (Sp / 16);
-    hipLaunchKernelGGL(jpeg_block_kernel, dim3(nblk), dim3(64), 0, st, raw, S, J, yp, cp);
+    hipLaunchKernelGGL(jpeg_block_kernel, dim3(nblk), dim3(64), 0, st, raw, S, P.jpeg_quality, yp, cp);
     hipLaunchKernelGGL(jpeg_rgb_kernel, grid, blk, 0, st, yp, cp, S, raw);
   }
   if (P.rain_n > 0) {

@@ -68,12 +68,14 @@ __global__ void bn_fold_kernel(const float* w, const float* b, const float* rm, 
 
 // train: stats = (sum, sumsq) over count values of z = conv + bias. Writes mean/rstd (for backward),
 // scale/shift (for apply) and updates running stats (momentum, unbiased var) like nn.BatchNorm2d.
-__global__ void bn_finalize_kernel(const double* stats, long count, const float* w, const float* b, float* rm, float* rv,
+// stats enter as the conv epilogue's fp64 [sum | sum of squares] and are cleared here (persistent workspace)
+__global__ void bn_finalize_kernel(double* stats, long count, const float* w, const float* b, float* rm, float* rv,
                                    float momentum, float eps, float* mean_o, float* rstd_o, float* scale, float* shift, int C) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   double mean = stats[c] / (double)count;
   double var = stats[C + c] / (double)count - mean * mean;
+  stats[c] = 0.0; stats[C + c] = 0.0;
   if (var < 0) var = 0;
   float rstd = (float)(1.0 / sqrt(var + (double)eps));
   mean_o[c] = (float)mean; rstd_o[c] = rstd;
@@ -192,12 +194,12 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const T* __restrict_
   }
 }
 
-// fold the replicas of [s1 | s2] into replica 0
+// fold the replicas of [s1 | s2] into replica 0 (replicas 1.. cleared as they are read)
 __global__ void bn_fold_replicas_kernel(double* sums, int C) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 2 * C) return;
   double s = sums[i];
-  for (int r = 1; r < S3OD_NREP; r++) s += sums[(long)r * 3 * C + i];
+  for (int r = 1; r < S3OD_NREP; r++) { s += sums[(long)r * 3 * C + i]; sums[(long)r * 3 * C + i] = 0.0; }
   sums[i] = s;
 }
 
@@ -262,16 +264,17 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
   }
 }
 
-__global__ void bn_param_grads_kernel(const double* sums, float* dw, float* db, float* dcb, int C) {
+// last reader of the BN backward workspace: clears what is left (replica 0's [s1 | s2], every replica's
+// conv-bias partials), so the workspace leaves all zero
+__global__ void bn_param_grads_kernel(double* sums, float* dw, float* db, float* dcb, int C) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   db[c] += (float)sums[c];
   dw[c] += (float)sums[C + c];
-  if (dcb) {
-    double s = 0.0;
-    for (int r = 0; r < S3OD_NREP; r++) s += sums[(long)r * 3 * C + 2 * C + c];
-    dcb[c] += (float)s;
-  }
+  sums[c] = 0.0; sums[C + c] = 0.0;
+  double s = 0.0;
+  for (int r = 0; r < S3OD_NREP; r++) { s += sums[(long)r * 3 * C + 2 * C + c]; sums[(long)r * 3 * C + 2 * C + c] = 0.0; }
+  if (dcb) dcb[c] += (float)s;
 }
 
 // ---------------------------------------------------------------- bilinear (align_corners=False)
@@ -562,7 +565,7 @@ int s3od_bn_fold(const float* w, const float* b, const float* rm, const float* r
   return s3od_check_launch("bn_fold");
 }
 
-int s3od_bn_finalize(const double* stats, long count, const float* w, const float* b, float* rm, float* rv, float momentum,
+int s3od_bn_finalize(double* stats, long count, const float* w, const float* b, float* rm, float* rv, float momentum,
                      float eps, float* mean, float* rstd, float* scale, float* shift, int C, void* stream) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, stats, count, w, b, rm, rv,
                      momentum, eps, mean, rstd, scale, shift, C);
@@ -579,13 +582,12 @@ int s3od_affine_act(int dtype, const void* x, const float* scale, const float* s
   return s3od_check_launch("affine_act");
 }
 
-// sums: workspace of S3OD_NREP * 3 * C doubles (replicated [s1 | s2 | conv-bias] accumulators)
+// sums: S3OD_NREP * 3 * C doubles (replicated [s1 | s2 | conv-bias] accumulators), all zero on entry; left all zero
 static int bn_bwd_impl(int dtype, const void* dy, const void* z, const void* y_relu, const float* as, const float* at,
                        const float* mean, const float* rstd, const float* w, double* sums, void* dz, float* dw, float* db,
                        float* dcb, long npix, int C, void* stream) {
   S3OD_REQUIRE(C % 8 == 0 && 256 % (C / 8) == 0, "bn_bwd: C");
   hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(sums, 0, sizeof(double) * S3OD_NREP * 3 * C, st);
   // blocks per pass (tools/hbm_bench.py bn, bs 16 x 256 channels): 1024 for >= 256K pixels (1M: 606 -> 542 us,
   // 256K: 173 -> 150 us), 512 below (64K: 1024 blocks of 64 pixels pay more in atomics: 61 -> 82 us)
   const int rows = 256 / (C / 8);

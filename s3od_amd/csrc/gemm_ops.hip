@@ -475,12 +475,16 @@ template <typename T, int BM, int BN, int NST> static int wgrad_split(int tiles,
 }
 
 // dw[(co*Cin + ci)*taps + tap] += ws[(co*taps + tap)*Cin + ci]   (one thread per dw element)
-__global__ void wgrad_permute_add_kernel(const float* __restrict__ ws, float* __restrict__ dw, int Cout, int Cin, int taps) {
+// ws enters all zero (split-K atomics land in it) and leaves all zero: each element is cleared as it is read,
+// so a persistent workspace needs no memset per call
+__global__ void wgrad_permute_add_kernel(float* __restrict__ ws, float* __restrict__ dw, int Cout, int Cin, int taps) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)Cout * Cin * taps) return;
   int tap = i % taps; long r = i / taps;
   int ci = r % Cin; int co = r / Cin;
-  dw[i] += ws[((long)co * taps + tap) * Cin + ci];
+  const long src = ((long)co * taps + tap) * Cin + ci;
+  dw[i] += ws[src];
+  ws[src] = 0.f;
 }
 
 extern "C" {
@@ -723,6 +727,7 @@ int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
 
 // conv wgrad: dw[Cout][Cin][KH][KW] (PyTorch layout, fp32) += sum_pix dy[pix][co] * x[src(pix,tap)][ci]
 // dy: [B,OH,OW,Cout]; x: [B,H,W,Cin].  Also serves ConvTranspose2d weights (conv view).
+// ws (nullable): Cout*KH*KW*Cin floats, all zero on entry and left all zero (split-K partials in the GEMM layout)
 int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW,
                     int stride, int pad, const void* dy, const void* x, int relu_x, float* dw, float* ws, int split,
                     void* stream) {
@@ -737,7 +742,6 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
   const int coblk = Cout % 64 == 0 ? 64 : (Cout == 96 ? 96 : 0);
   if (wg_knob && dtype == S3OD_BF16 && ws && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W &&
       Cin % 64 == 0 && coblk && (Cin == 64 || (long)H * W >= 512L * 512)) {
-    (void)hipMemsetAsync(ws, 0, sizeof(float) * (size_t)M * N, st);
     int rc = coblk == 64 ? (relu_x ? launch_wgrad_halo<64, true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)
                                    : launch_wgrad_halo<64, false>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st))
                          : (relu_x ? launch_wgrad_halo<96, true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)
@@ -756,7 +760,6 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
       // taps > 1: the split-K atomics go to a workspace in the GEMM's own [Cout][tap][Cin] layout
       // (a wave's adds hit contiguous addresses), then one pass permutes into the PyTorch layout
       const bool viaws = ws != nullptr && KH * KW > 1;
-      if (viaws) (void)hipMemsetAsync(ws, 0, sizeof(float) * (size_t)M * N, st);
       EpiWgrad e = viaws ? EpiWgrad{ws, M, N, N, 1} : EpiWgrad{dw, M, N, Cin, KH * KW};
       int rc = launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST>(la, lb, e, M, N, KTILES, sp, 1, st);
       if (rc || !viaws) return rc;

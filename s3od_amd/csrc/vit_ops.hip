@@ -171,11 +171,12 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
 }
 
 // a[i] += sum_r ws[r][i], b[i] += sum_r ws[r][D + i]   (fold of the replicated 2 x D partials; a/b may be null)
-__global__ void fold2_kernel(const float* __restrict__ ws, float* __restrict__ a, float* __restrict__ b, int D) {
+// sums the S3OD_NREP replicas of [a | b] partials and clears them (the workspace enters and leaves all zero)
+__global__ void fold2_kernel(float* __restrict__ ws, float* __restrict__ a, float* __restrict__ b, int D) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 2 * D) return;
   float s = 0.f;
-  for (int r = 0; r < S3OD_NREP; r++) s += ws[(long)r * 2 * D + i];
+  for (int r = 0; r < S3OD_NREP; r++) { s += ws[(long)r * 2 * D + i]; ws[(long)r * 2 * D + i] = 0.f; }
   if (i < D) { if (a) a[i] += s; }
   else if (b) b[i - D] += s;
 }
@@ -375,12 +376,11 @@ int s3od_layernorm_fwd(int dtype, const float* x, const float* w, const float* b
   return s3od_check_launch("layernorm_fwd");
 }
 
-// ws: workspace of S3OD_NREP * 2 * D floats (replicated dw / db partials)
+// ws: S3OD_NREP * 2 * D floats (replicated dw / db partials), all zero on entry; left all zero
 int s3od_layernorm_bwd(int dtype, const void* dy, const float* x, const float* mean, const float* rstd, const float* w,
                        const float* dres, float* dx, float* dw, float* db, float* ws, int M, int D_, void* stream) {
   static const int rpb = dev_knob("S3OD_LN_RPB", 32);
   hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(ws, 0, sizeof(float) * S3OD_NREP * 2 * D_, st);
   DISPATCH_D(D_, {
     DISPATCH_T(dtype, {
       hipLaunchKernelGGL((ln_bwd_kernel<T, D>), dim3(cdiv(M, rpb)), dim3(256), 0, st, (const T*)dy, x, mean, rstd, w, dres, dx, ws, M, rpb);
@@ -410,12 +410,11 @@ int s3od_colsum(int dtype, const void* a, long lda, int M, int N, float* out, vo
   return s3od_check_launch("colsum");
 }
 
-// ws: workspace of S3OD_NREP * 2 * D floats (replicated dlam / dbias partials)
+// ws: S3OD_NREP * 2 * D floats (replicated dlam / dbias partials), all zero on entry; left all zero
 int s3od_layerscale_bwd(int dtype, const float* dx, const void* u, const float* lam, void* du, float* dlam, float* dbias,
                         float* ws, int M, int D_, void* stream) {
   static const int rpb = dev_knob("S3OD_LS_RPB", 16);
   hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(ws, 0, sizeof(float) * S3OD_NREP * 2 * D_, st);
   DISPATCH_D(D_, {
     DISPATCH_T(dtype, {
       hipLaunchKernelGGL((scale_bwd_kernel<T, D>), dim3(cdiv(M, rpb)), dim3(D / 2), 0, st, dx, (const T*)u, lam, (T*)du, ws, M, rpb);
@@ -425,7 +424,7 @@ int s3od_layerscale_bwd(int dtype, const float* dx, const void* u, const float* 
   return s3od_check_launch("layerscale_bwd");
 }
 
-// H heads of 64 (D = 64 H); ws: S3OD_NREP * 2 * D floats
+// H heads of 64 (D = 64 H); ws: S3OD_NREP * 2 * D floats, all zero on entry; left all zero
 int s3od_qkv_unrope(int dtype, const void* dq, const void* dk, const void* dv, const float* cs, const float* sn,
                     void* dqkv, float* dbq, float* dbv, float* ws, int B, int Ntok, int P, int H, void* stream) {
   S3OD_REQUIRE(ws || (!dbq && !dbv), "qkv_unrope: bias gradients need the workspace");
@@ -434,7 +433,6 @@ int s3od_qkv_unrope(int dtype, const void* dq, const void* dk, const void* dv, c
   const int D_ = 64 * H;
   const int rpb = dev_knob("S3OD_UNROPE_RPB", 64);
   hipStream_t st = (hipStream_t)stream;
-  if (ws) (void)hipMemsetAsync(ws, 0, sizeof(float) * S3OD_NREP * 2 * D_, st);
   DISPATCH_T(dtype, {
     if (H == 12)
       hipLaunchKernelGGL((qkv_unrope_kernel<T, 12>), dim3(cdiv(M, rpb)), dim3(24 * 12), 0, st, (const T*)dq, (const T*)dk,

@@ -52,6 +52,18 @@ class DPTEngine:
         self.set_dtype(compute_dtype)
         self.w = {}
         self._wkey = None
+        self._zpool = {}       # persistent all-zero workspaces (the kernels that read them back leave them zero)
+        self._nbt = []         # BatchNorm num_batches_tracked counters to bump once per forward
+
+    def zero_ws(self, key, n, dtype, dev):
+        """Persistent workspace of >= n elements that is all zero between calls: every C-ABI entry given one
+        (replicated column sums, BN statistics, split-K wgrad partials) clears what it reads back, so no
+        memset is launched per call.  One buffer per key; all users run on one stream, in order."""
+        t = self._zpool.get(key)
+        if t is None or t.numel() < n or t.dtype != dtype or t.device != dev:
+            t = torch.zeros(n, dtype=dtype, device=dev)
+            self._zpool[key] = t
+        return t
 
     def set_dtype(self, compute_dtype):
         assert compute_dtype in ("bf16", "f32")
@@ -294,7 +306,7 @@ class DPTEngine:
         return out
 
     def _conv_bn_train(self, x, wt, B, h, w, bias, relu_in=False):
-        stats = torch.zeros(2 * 256, dtype=torch.float64, device=x.device)
+        stats = self.zero_ws("bn_stats", 2 * 256, torch.float64, x.device)   # cleared by s3od_bn_finalize
         z = self._conv(x, wt, B, h, w, 256, 256, 3, 1, 1, bias=bias, relu_in=relu_in, stats=stats)
         return dict(z=z, stats=stats)
 
@@ -305,7 +317,7 @@ class DPTEngine:
               self.buf[name + ".running_var"], 0.1, 1e-5, d["mean"], d["rstd"], d["scale"], d["shift"], 256, stream())
         nbt = self.buf.get(name + ".num_batches_tracked")
         if nbt is not None:
-            nbt.add_(1)
+            self._nbt.append(nbt)      # bumped together at the end of the forward (one launch)
         return d
 
     def _bnfold(self, name, st):
@@ -393,7 +405,11 @@ class DPTEngine:
         taps, (B, ph, pw, Nt) = self.encoder_forward(x, train, rope_rescale, ctx)
         if ctx is not None:
             ctx.B, ctx.H, ctx.W, ctx.ph, ctx.pw = B, x.shape[2], x.shape[3], ph, pw
-        return self.decoder_forward(taps, B, ph, pw, train, ctx)
+        out = self.decoder_forward(taps, B, ph, pw, train, ctx)
+        if self._nbt:
+            torch._foreach_add_(self._nbt, 1)
+            self._nbt = []
+        return out
 
     # ================================================================== backward
     def _colsum(self, a, M, N, out, lda=None):
@@ -408,8 +424,8 @@ class DPTEngine:
               row_mode, P, prefix, colsum, stream())
 
     def _wgrad_conv(self, dy, x, B, H, W, Cin, OH, OW, Cout, k, s, p, dw, relu_x=False):
-        # taps > 1: fp32 workspace in the GEMM's [Cout][tap][Cin] layout (contiguous split-K atomics)
-        ws = torch.empty(Cout * k * k * Cin, dtype=torch.float32, device=dy.device) if k > 1 else None
+        # taps > 1: fp32 workspace in the GEMM's [Cout][tap][Cin] layout (contiguous split-K atomics), zero between calls
+        ws = self.zero_ws("wgrad", Cout * k * k * Cin, torch.float32, dy.device) if k > 1 else None
         lib()("s3od_conv_wgrad", self.dt, B, H, W, Cin, OH, OW, Cout, k, k, s, p, dy, x, int(relu_x), dw, ws, 0, stream())
 
     def _dgrad_conv(self, dy, w, B, H, W, Cin, OH, OW, Cout, k, s, p, act=ACT_NONE, res1=None, out=None, colsum=None,
@@ -439,7 +455,7 @@ class DPTEngine:
         h, w = c["h"], c["w"]
         npix = B * h * w
         dev = d_out.device
-        sums = torch.empty(32 * 3 * 256, dtype=torch.float64, device=dev)   # S3OD_NREP replicas
+        sums = self.zero_ws("bn_sums", 32 * 3 * 256, torch.float64, dev)   # S3OD_NREP replicas, zero between calls
         dz2 = torch.empty_like(d_out)
         L("s3od_bn_bwd", self.dt, d_out, c["z2"], None, c["bn2"]["mean"], c["bn2"]["rstd"], P[q + "bn2.weight"], sums, dz2,
           G[q + "bn2.weight"], G[q + "bn2.bias"], G[q + "conv2.bias"], npix, 256, st)
@@ -558,7 +574,10 @@ class DPTEngine:
         Nt = NP + 1 + NREG
         M = B * Nt
         dev = dtaps[0][0].device
-        dx = torch.zeros((B, Nt, D), dtype=torch.float32, device=dev)
+        # the first tap gradient writes the patch rows; only the prefix rows (cls + registers) need zeros
+        dx = torch.empty((B, Nt, D), dtype=torch.float32, device=dev)
+        dx[:, :1 + NREG].zero_()
+        first_tap = True
         tap_of = {t: j for j, t in enumerate(self.taps)}
         du = _E(None, (M, D), T, dev)
         dhp = _E(None, (M, MLP), T, dev)
@@ -567,14 +586,15 @@ class DPTEngine:
         dxi = _E(None, (B, Nt, D), torch.float32, dev)
         dqkv = _E(None, (M, 3 * D), T, dev)
         delta = _E(None, (B * H, Nt), torch.float32, dev)
-        qv_ws = _E(None, (32 * 2 * D,), torch.float32, dev)     # S3OD_NREP replicas of the q/v bias partials
-        red_ws = _E(None, (32 * 2 * D,), torch.float32, dev)    # same, for LayerNorm / LayerScale parameter grads
+        qv_ws = self.zero_ws("qv", 32 * 2 * D, torch.float32, dev)     # S3OD_NREP replicas of the q/v bias partials
+        red_ws = self.zero_ws("red", 32 * 2 * D, torch.float32, dev)   # same, for LayerNorm / LayerScale parameter grads
         for i in reversed(range(self.last)):
             if i + 1 in tap_of:
                 dp, c = dtaps[tap_of[i + 1]]
                 # dx[prefix-skipped rows] += dproj @ W_proj   (in-place accumulate, fp32)
-                self._dgrad_lin(dp, W8[f"proj{tap_of[i + 1]}"], B * NP, D, c, dx, aux=dx, out_f32=True,
-                                row_mode=1, P=NP, prefix=1 + NREG, ldaux=D)
+                self._dgrad_lin(dp, W8[f"proj{tap_of[i + 1]}"], B * NP, D, c, dx, aux=None if first_tap else dx,
+                                out_f32=True, row_mode=1, P=NP, prefix=1 + NREG, ldaux=D)
+                first_tap = False
             p = f"encoder.model.layer.{i}."
             s = ctx.t[f"L{i}"]
             # ---- MLP half

@@ -121,14 +121,18 @@ def test_attn_bwd_qkv_fused_equals_separate_path():
     sn = torch.cat([th.sin(), th.sin()], 1).contiguous()
     delta = torch.empty(B * H, N, device="cuda")
     dq, dk, dv = (torch.empty(B * H, N, 64, device="cuda", dtype=torch.bfloat16) for _ in range(3))
-    ws = torch.empty(32 * 2 * D, device="cuda")
+    ws = torch.zeros(32 * 2 * D, device="cuda")                 # contract: all zero on entry, left all zero
     a = torch.empty(B * N, 3 * D, device="cuda", dtype=torch.bfloat16)
     bq_a, bv_a = torch.zeros(D, device="cuda"), torch.zeros(D, device="cuda")
     lib()("s3od_attn_bwd", 1, q, k, v, o, do, lse, delta, dq, dk, dv, B, H, N, stream())
     lib()("s3od_qkv_unrope", 1, dq, dk, dv, cs, sn, a, bq_a, bv_a, ws, B, N, P, H, stream())
+    torch.cuda.synchronize()
+    assert int((ws != 0).sum()) == 0, "qkv_unrope must leave its workspace all zero"
     f = torch.empty_like(a)
     bq_f, bv_f = torch.zeros(D, device="cuda"), torch.zeros(D, device="cuda")
     lib()("s3od_attn_bwd_qkv", 1, q, k, v, o, do, lse, delta, cs, sn, P, f, bq_f, bv_f, ws, B, H, N, stream())
+    torch.cuda.synchronize()
+    assert int((ws != 0).sum()) == 0, "attn_bwd_qkv must leave its workspace all zero"
     torch.cuda.synchronize()
     af, ff = a.float(), f.float()
     assert float((af - ff).abs().max() / af.abs().max()) < 1e-2

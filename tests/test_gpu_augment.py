@@ -3,10 +3,12 @@ against oracle/augment_oracle.py, the numpy restatement of albumentations 2.0.8 
 algorithms (neither library is installed: parity with them is unpinned; these tests pin the kernels to
 the restated algorithms).  Each member runs alone through the C ABI on a seeded [0,1] image:
 
-* CLAHE (8x8 tiles, clip 2.5) and ISONoise: the 8-bit L / Poisson draws can flip on float32-vs-float64
-  rounding, so <= 0.2 % of pixels may differ by more than 1e-3 (CLAHE: float32 Lab round trip) / 1e-4;
-* ImageCompression at quality 30 / 75 and a canvas that is not a multiple of the 16-pixel MCU: <= 0.5 %
-  of pixels more than one 8-bit step away, mean |d| <= 2e-3;
+* CLAHE (8x8 tiles, clip 2.5): an 8-bit L value on a rounding tie of the LUT interpolation may flip by one
+  step (float32 on device, float64 here): <= 1.5 % of pixels beyond 1e-3, max <= 0.02, mean <= 3e-4;
+* ISONoise: a Poisson draw on the inversion boundary may flip: <= 0.2 % of pixels beyond 1e-4;
+* ImageCompression at quality 30 / 55 / 75 and a canvas that is not a multiple of the 16-pixel MCU: a
+  coefficient whose quantisation rounds the other way (float32 DCT on device, float64 here) moves its
+  8x8 block, so <= 3 % of pixels may be more than one 8-bit step away, mean |d| <= 1e-3;
 * ZoomBlur (+ Sharpen composed), Downscale + RandomBrightnessContrast, RandomShadow, RandomSnow,
   RandomRain, GridDistortion, ElasticTransform: <= 1e-4 (shadow / snow: <= 0.1 % of pixels on a
   polygon edge / threshold may differ);
@@ -58,8 +60,10 @@ def test_clahe(S):
     q.clahe_clip = 2.5
     got = _run(x, q)
     ref = AO.clahe(x.cpu().numpy().astype(np.float64), 2.5)
-    # float32 Lab round trip on device (~1e-4 near black) vs float64 here; flipped 8-bit L values
-    assert _frac(got, ref, 1e-3) <= 2e-3 and np.abs(got - ref).max() < 0.05, (_frac(got, ref, 1e-3), np.abs(got - ref).max())
+    # float32 Lab round trip on device (~1e-4 near black) vs float64 here; an 8-bit L value whose LUT
+    # interpolation lands on a rounding tie (common with 12-pixel tiles) may flip by one step (<= 2.5/255 in RGB)
+    d = np.abs(got - ref)
+    assert _frac(got, ref, 1e-3) <= 1.5e-2 and d.max() < 0.02 and d.mean() < 3e-4, (_frac(got, ref, 1e-3), d.max(), d.mean())
     assert np.abs(got - x.cpu().numpy()).mean() > 1e-3          # the member did something
 
 
@@ -85,7 +89,7 @@ def test_jpeg(S, quality):
     got = _run(x, q)
     ref = AO.jpeg(x.cpu().numpy().astype(np.float64), quality)
     f = _frac(got, ref, 1.5 / 255)
-    assert f <= 5e-3 and np.abs(got - ref).mean() <= 2e-3, (f, np.abs(got - ref).mean())
+    assert f <= 3e-2 and np.abs(got - ref).mean() <= 1e-3, (f, np.abs(got - ref).mean())
     assert np.abs(got - x.cpu().numpy()).mean() > 1e-3
 
 

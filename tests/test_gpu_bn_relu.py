@@ -43,7 +43,7 @@ def test_bn_relu_bwd_matches_stored_mask(dtype):
 
     outs = []
     for mode in ("stored", "recompute"):
-        sums = torch.empty(32 * 3 * C, dtype=torch.float64, device=dev)
+        sums = torch.zeros(32 * 3 * C, dtype=torch.float64, device=dev)     # all zero on entry, left all zero
         dz = torch.empty_like(z)
         dw, db, dcb = (torch.zeros(C, device=dev) for _ in range(3))
         if mode == "stored":
@@ -51,6 +51,7 @@ def test_bn_relu_bwd_matches_stored_mask(dtype):
         else:
             L("s3od_bn_relu_bwd", code, dy, z, scale, shift, mean, rstd, w, sums, dz, dw, db, dcb, npix, C, st)
         torch.cuda.synchronize()
+        assert int((sums != 0).sum()) == 0, "bn backward must leave its workspace all zero"
         outs.append((dz, dw, db, dcb))
     n_edge = int(((y[: npix // 4].float() == 0) & (z[: npix // 4].float() * scale + shift >= -1e-3)).sum())
     assert n_edge > 0

@@ -96,9 +96,10 @@ def test_conv_wgrad_halo(cout, B, H, W, relu):
     ref = torch.nn.grad.conv2d_weight(xin, (cout, 64, 3, 3), dy.float(), padding=1)
     dw0 = torch.randn(cout, 64, 3, 3, device="cuda", generator=g)
     dw = dw0.clone()
-    ws = torch.empty(cout * 9 * 64, device="cuda")
+    ws = torch.zeros(cout * 9 * 64, device="cuda")                 # all zero on entry, left all zero
     lib()("s3od_conv_wgrad", BF16, B, H, W, 64, H, W, cout, 3, 3, 1, 1, _nhwc(dy), _nhwc(x), int(relu), dw, ws, 0, stream())
     torch.cuda.synchronize()
+    assert int((ws != 0).sum()) == 0, "conv_wgrad must leave its workspace all zero"
     got = dw - dw0
     assert float((got - ref).abs().max() / ref.abs().max()) < 2e-3, float((got - ref).abs().max() / ref.abs().max())
 
@@ -115,7 +116,8 @@ def test_conv_wgrad_halo_channel_blocks(cin, cout, B, H, W, relu):
     xin = F.relu(x.float()) if relu else x.float()
     ref = torch.nn.grad.conv2d_weight(xin, (cout, cin, 3, 3), dy.float(), padding=1)
     dw = torch.zeros(cout, cin, 3, 3, device="cuda")
-    ws = torch.empty(cout * 9 * cin, device="cuda")
+    ws = torch.zeros(cout * 9 * cin, device="cuda")                # all zero on entry, left all zero
     lib()("s3od_conv_wgrad", BF16, B, H, W, cin, H, W, cout, 3, 3, 1, 1, _nhwc(dy), _nhwc(x), int(relu), dw, ws, 0, stream())
     torch.cuda.synchronize()
+    assert int((ws != 0).sum()) == 0, "conv_wgrad must leave its workspace all zero"
     assert float((dw - ref).abs().max() / ref.abs().max()) < 2e-3, float((dw - ref).abs().max() / ref.abs().max())

@@ -15,7 +15,7 @@ def bn_bwd(npix=16 * 256 * 256, C=256, relu=True):
     z = torch.randn_like(dy)
     y = torch.randn_like(dy) if relu else None
     mean = torch.zeros(C, device="cuda"); rstd = torch.ones(C, device="cuda"); w = torch.ones(C, device="cuda")
-    sums = torch.empty(32 * 3 * C, dtype=torch.float64, device="cuda")
+    sums = torch.zeros(32 * 3 * C, dtype=torch.float64, device="cuda")
     dz = torch.empty_like(dy)
     dw, db, dcb = (torch.zeros(C, device="cuda") for _ in range(3))
     f = lambda: lib()("s3od_bn_bwd", BF16, dy, z, y, mean, rstd, w, sums, dz, dw, db, dcb, npix, C, stream())
@@ -30,7 +30,7 @@ def bn_relu_bwd(npix=16 * 256 * 256, C=256):
     z = torch.randn_like(dy)
     mean = torch.zeros(C, device="cuda"); rstd = torch.ones(C, device="cuda"); w = torch.ones(C, device="cuda")
     sc, sh = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
-    sums = torch.empty(32 * 3 * C, dtype=torch.float64, device="cuda")
+    sums = torch.zeros(32 * 3 * C, dtype=torch.float64, device="cuda")
     dz = torch.empty_like(dy)
     dw, db, dcb = (torch.zeros(C, device="cuda") for _ in range(3))
     f = lambda: lib()("s3od_bn_relu_bwd", BF16, dy, z, sc, sh, mean, rstd, w, sums, dz, dw, db, dcb, npix, C, stream())
@@ -45,7 +45,7 @@ def unrope(B=16, N=4101):
     cs = torch.randn(N - 5, 64, device="cuda"); sn = torch.randn_like(cs)
     out = torch.empty(B * N, 2304, device="cuda", dtype=torch.bfloat16)
     bq, bv = torch.zeros(768, device="cuda"), torch.zeros(768, device="cuda")
-    ws = torch.empty(32 * 1536, device="cuda")
+    ws = torch.zeros(32 * 1536, device="cuda")
     f = lambda: lib()("s3od_qkv_unrope", BF16, dq, dk, dv, cs, sn, out, bq, bv, ws, B, N, N - 5, stream())
     t = timeit(f)
     nbytes = 2 * out.numel() * 2
@@ -59,7 +59,7 @@ def vit_bwd(M=16 * 4101, D=768):
     x = torch.randn(M, D, device="cuda"); dres = torch.randn_like(x); dx = torch.empty_like(x)
     mean = x.mean(1); rstd = torch.ones(M, device="cuda"); w = torch.ones(D, device="cuda")
     dw, db = torch.zeros(D, device="cuda"), torch.zeros(D, device="cuda")
-    ws = torch.empty(32 * 2 * D, device="cuda")
+    ws = torch.zeros(32 * 2 * D, device="cuda")
     t = timeit(lambda: lib()("s3od_layernorm_bwd", BF16, dy, x, mean, rstd, w, dres, dx, dw, db, ws, M, D, stream()))
     nb = M * D * (2 + 4 + 4 + 4)
     print(f"layernorm_bwd M={M} D={D}: {t * 1e6:8.1f} us  {nb / t / 1e12:6.2f} TB/s")

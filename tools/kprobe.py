@@ -25,7 +25,7 @@ if which in ("wgrad64", "conv64"):
     x = torch.randn(B, H, H, C, device="cuda").bfloat16()
     w = torch.randn(C, 3, 3, C, device="cuda").bfloat16()
     dw = torch.zeros(C * 9 * C, device="cuda")
-    ws = torch.empty(C * 9 * C, device="cuda")
+    ws = torch.zeros(C * 9 * C, device="cuda")
     out = torch.empty_like(x)
     for _ in range(3):
         if which == "wgrad64":

@@ -87,7 +87,7 @@ def dgrad_conv(name, B, H, Cin, Cout, k=3):
 def wgrad_conv(name, B, H, Cin, Cout):
     dy, x = r(B, H, H, Cout), r(B, H, H, Cin)
     dw = torch.zeros(Cout * 9 * Cin, device="cuda")
-    ws = torch.empty(Cout * 9 * Cin, device="cuda")
+    ws = torch.zeros(Cout * 9 * Cin, device="cuda")
     f = lambda: lib()("s3od_conv_wgrad", BF16, B, H, H, Cin, H, H, Cout, 3, 3, 1, 1, dy, x, 0, dw, ws, 0, stream())
     report(name, 2.0 * B * H * H * Cout * Cin * 9, timeit(f))
 
