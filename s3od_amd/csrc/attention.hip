@@ -864,24 +864,65 @@ DEV void qkv_colsum32(const QkvSink& o, int which, int hh, int H, int rep, int l
 }
 }  // namespace
 
-// dK, dV.  Workgroup = W waves x 32 keys of one (b,h); loop over 64-query tiles (Q, dO, -LSE, -delta staged
-// in double-buffered LDS, one barrier per tile).
-template <int W>
+// LDS-DMA of a 64-row x 128-B tile into an Img32 (buffer_load_dwordx4 ... lds: one wave instruction fills 1 KiB
+// of LDS lane-linearly, so the image's XOR swizzle is applied to each lane's SOURCE chunk), W waves.  Rows past
+// the buffer's end read zeros (hardware range check), so tile tails need no masking.
+typedef __attribute__((address_space(3))) void lds_void;
+DEV __amdgpu_buffer_rsrc_t attn_rsrc(const void* p, unsigned long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(unsigned)bytes, 0x00020000);
+}
+template <int W> struct Dma64 {
+  static constexpr int NIW = 8 / W;
+  // stage rows row0 .. row0+63 (row stride ldb bytes) of buffer r into the image at `img`
+  DEV static void issue(__amdgpu_buffer_rsrc_t r, long row0, long ldb, char* img, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < NIW; i++) {
+      const int o = (wave * NIW + i) * 1024 + lane * 16, row = o >> 7, lc = ((o >> 4) & 7) ^ Img32::sw(row);
+      const long src = (row0 + row) * ldb + lc * 16;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(img + (wave * NIW + i) * 1024), 16,
+                                               src < 0x7FFFFFFFL ? (unsigned)src : 0x80000000u, 0, 0, 0);
+    }
+  }
+};
+// 64 fp32 row constants (LSE or delta of one 64-query tile) by one wave's LDS-DMA (lanes 0..15 carry data)
+DEV void dma_row64(__amdgpu_buffer_rsrc_t r, long q0, char* dst, int lane) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, lane < 16 ? (unsigned)((q0 + 4 * lane) * 4) : 0x80000000u, 0, 0, 0);
+}
+DEV f32x16 ld16(const float* p) {      // 4 consecutive-row groups of the 32x32 C layout (rows 8m + 0..3)
+  const f32x4 a = *(const f32x4*)(p), b = *(const f32x4*)(p + 8), c = *(const f32x4*)(p + 16), d = *(const f32x4*)(p + 24);
+  return f32x16{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3], c[0], c[1], c[2], c[3], d[0], d[1], d[2], d[3]};
+}
+DEV bf16x8 neg8(bf16x8 v) {
+  bf16x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; e++) r[e] = (bf16)(-(float)v[e]);
+  return r;
+}
+
+// dK, dV.  Workgroup = W waves x 32 keys of one (b,h); loop over 64-query tiles.  Q, dO, LSE and delta of the
+// next tile arrive by LDS-DMA during the current one (two LDS stages, one barrier per tile).  Signs: the key
+// and value fragments are held negated, so the accumulators start at +LSE / +delta straight from LDS and hold
+// LSE - S and delta - dP (exp2 takes the negation for free as an input modifier); dS is carried negated and
+// flipped at the store.
+// PRIO: the second half of the workgroup's waves run at s_setprio 1 (MI355X_MICROARCH "Two waves per SIMD" item 4)
+// IL: interleave the softmax VALU of one 32-query half between the other half's MFMAs (sched_group_barrier)
+template <int W, bool PRIO, bool IL>
 __global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                                    const bf16* __restrict__ V, const bf16* __restrict__ dO,
                                                                    const float* __restrict__ LSE, const float* __restrict__ Dl,
                                                                    bf16* __restrict__ dK, bf16* __restrict__ dV, int N, int H,
                                                                    QkvSink sink) {
-  constexpr int NT = 64 * W, SB = 2 * Img32::BYTES + 512;
-  __shared__ __attribute__((aligned(16))) char smem[2 * SB];
+  constexpr int SB = 2 * Img32::BYTES + 2048;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * SB];
   const int bh = blockIdx.y, b = bh / H, hh = bh - b * H;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const bf16* Qp = Q + (long)bh * N * 64;
-  const bf16* dOp = dO + (long)b * N * (H * 64) + hh * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5;
   const long ldo = (long)H * 64;
-  const float* Lp = LSE + (long)bh * N;
-  const float* Dp = Dl + (long)bh * N;
+  const auto rq = attn_rsrc(Q + (long)bh * N * 64, (unsigned long)N * 128);
+  const auto rdo = attn_rsrc(dO + (long)b * N * ldo + hh * 64, ((unsigned long)(N - 1) * ldo + 64) * 2);
+  const auto rl = attn_rsrc(LSE + (long)bh * N, (unsigned long)N * 4);
+  const auto rd = attn_rsrc(Dl + (long)bh * N, (unsigned long)N * 4);
   const int k0 = blockIdx.x * (32 * W) + wave * 32;
+  if (PRIO && wave >= W / 2) __builtin_amdgcn_s_setprio(1);
   bf16x8 kf[4], vf[4];
   {
     const int key = k0 + (lane & 31);
@@ -890,79 +931,87 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __r
     bf16x8 z; for (int e = 0; e < 8; e++) z[e] = (bf16)0.f;
 #pragma unroll
     for (int ks = 0; ks < 4; ks++) {
-      kf[ks] = key < N ? *(const bf16x8*)(kr + 16 * ks) : z;
-      vf[ks] = key < N ? *(const bf16x8*)(vr + 16 * ks) : z;
+      kf[ks] = key < N ? neg8(*(const bf16x8*)(kr + 16 * ks)) : z;
+      vf[ks] = key < N ? neg8(*(const bf16x8*)(vr + 16 * ks)) : z;
     }
   }
   f32x16 dk[2], dv[2];
 #pragma unroll
   for (int db = 0; db < 2; db++) for (int i = 0; i < 16; i++) { dk[db][i] = 0.f; dv[db][i] = 0.f; }
-  RowTile32<NT> tq, tdo;
-  float lse_r = 0.f, dl_r = 0.f;
   const int nqt = (N + 63) / 64;
-  auto stage_load = [&](int qt) {
-    tq.load(Qp, 64, qt * 64, N, tid);
-    tdo.load(dOp, ldo, qt * 64, N, tid);
-    if (tid < 64) { const int q = qt * 64 + tid; lse_r = q < N ? -Lp[q] : -INFINITY; dl_r = q < N ? -Dp[q] : 0.f; }
+  auto stage = [&](int qt, char* base) {
+    Dma64<W>::issue(rq, (long)qt * 64, 128, base, wave, lane);
+    Dma64<W>::issue(rdo, (long)qt * 64, ldo * 2, base + Img32::BYTES, wave, lane);
+    if (wave == 0) dma_row64(rl, (long)qt * 64, base + 2 * Img32::BYTES, lane);
+    if (wave == W - 1) dma_row64(rd, (long)qt * 64, base + 2 * Img32::BYTES + 1024, lane);
   };
-  auto stage_store = [&](char* base) {
-    tq.store(base, tid); tdo.store(base + Img32::BYTES, tid);
-    if (tid < 64) { ((float*)(base + 2 * Img32::BYTES))[tid] = lse_r; ((float*)(base + 2 * Img32::BYTES))[64 + tid] = dl_r; }
-  };
-  stage_load(0);
-  stage_store(smem);
+  stage(0, smem);
   __syncthreads();
   int cur = 0;
   for (int qt = 0; qt < nqt; qt++) {
-    const bool more = qt + 1 < nqt;
-    if (more) stage_load(qt + 1);
+    if (qt + 1 < nqt) stage(qt + 1, smem + (cur ^ 1) * SB);
     const char* qs_ = smem + cur * SB;
     const char* dos = qs_ + Img32::BYTES;
     const float* lsel = (const float*)(qs_ + 2 * Img32::BYTES);
-    const float* dll = lsel + 64;
+    const float* dll = (const float*)(qs_ + 2 * Img32::BYTES + 1024);
+    // software-pipelined over the two 32-query halves: the softmax VALU of one half is scheduled between the
+    // MFMAs of the other (sched_group_barrier), so the matrix pipe does not idle through the exp / pack work
     f32x16 s[2], dp[2];
+    bf16x8 pa[2][2], da[2][2];
+    auto sdp = [&](int qb) {
+      bf16x8 a[4], c[4];
 #pragma unroll
-    for (int qb = 0; qb < 2; qb++) {
+      for (int ks = 0; ks < 4; ks++) { a[ks] = row32(qs_, 32 * qb, ks, lane); c[ks] = row32(dos, 32 * qb, ks, lane); }
+      s[qb] = mma32(a[0], kf[0], ld16(lsel + 32 * qb + 4 * h));
+      dp[qb] = mma32(c[0], vf[0], ld16(dll + 32 * qb + 4 * h));
 #pragma unroll
-      for (int m = 0; m < 4; m++) {   // C = -LSE / -delta of rows 32qb + 8m + 4h + 0..3 (broadcast reads)
-        const f32x4 nl = *(const f32x4*)(lsel + 32 * qb + 8 * m + 4 * h), nd = *(const f32x4*)(dll + 32 * qb + 8 * m + 4 * h);
-#pragma unroll
-        for (int e = 0; e < 4; e++) { s[qb][4 * m + e] = nl[e]; dp[qb][4 * m + e] = nd[e]; }
-      }
-#pragma unroll
-      for (int ks = 0; ks < 4; ks++) {
-        s[qb] = mma32(row32(qs_, 32 * qb, ks, lane), kf[ks], s[qb]);
-        dp[qb] = mma32(row32(dos, 32 * qb, ks, lane), vf[ks], dp[qb]);
-      }
-    }
-    // P = exp2(S - LSE[q]); dS = P (dP - delta[q])   (invalid q: -LSE = -inf -> P = 0)
-#pragma unroll
-    for (int qb = 0; qb < 2; qb++)
+      for (int ks = 1; ks < 4; ks++) { s[qb] = mma32(a[ks], kf[ks], s[qb]); dp[qb] = mma32(c[ks], vf[ks], dp[qb]); }
+    };
+    // s = LSE - S, dp = delta - dP:  P = exp2(-s);  -dS = P * dp ; packed as the A operands of dV / dK
+    auto softmax = [&](int qb) {
 #pragma unroll
       for (int i = 0; i < 16; i++) {
-        const float p = fexp2(s[qb][i]);
+        const float p = fexp2(-s[qb][i]);
         s[qb][i] = p;
         dp[qb][i] *= p;
       }
-    // dV += P^T dO ; dK += dS^T Q   (k = query: 4 steps of 16)
 #pragma unroll
-    for (int qb = 0; qb < 2; qb++)
+      for (int st = 0; st < 2; st++) { pa[qb][st] = pack_acc(s[qb], st); da[qb][st] = pack_acc(dp[qb], st); }
+    };
+    auto dvdk = [&](int qb) {
 #pragma unroll
       for (int st = 0; st < 2; st++) {
-        const bf16x8 pa = pack_acc(s[qb], st), da = pack_acc(dp[qb], st);
+        bf16x8 bo[2], bq[2];
 #pragma unroll
-        for (int db = 0; db < 2; db++) {
-          dv[db] = mma32(pa, tr32(dos, 32 * qb + 16 * st, 32 * db, lane), dv[db]);
-          dk[db] = mma32(da, tr32(qs_, 32 * qb + 16 * st, 32 * db, lane), dk[db]);
-        }
+        for (int db = 0; db < 2; db++) { bo[db] = tr32(dos, 32 * qb + 16 * st, 32 * db, lane); bq[db] = tr32(qs_, 32 * qb + 16 * st, 32 * db, lane); }
+#pragma unroll
+        for (int db = 0; db < 2; db++) { dv[db] = mma32(pa[qb][st], bo[db], dv[db]); dk[db] = mma32(da[qb][st], bq[db], dk[db]); }
       }
-    if (more) stage_store(smem + (cur ^ 1) * SB);
-    __syncthreads();
+    };
+    auto interleave = [&]() {      // 8 MFMAs, each followed by up to 6 VALU (the other half's softmax)
+#pragma unroll
+      for (int g = 0; g < 8; g++) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+      }
+    };
+    sdp(0);
+    __builtin_amdgcn_sched_barrier(0);
+    sdp(1);
+    softmax(0);
+    if (IL) interleave();
+    __builtin_amdgcn_sched_barrier(0);
+    dvdk(0);
+    softmax(1);
+    if (IL) interleave();
+    __builtin_amdgcn_sched_barrier(0);
+    dvdk(1);
+    __syncthreads();      // drains this tile's reads and the next tile's LDS-DMA (vmcnt(0)) before the flip
     cur ^= 1;
   }
   if (sink.dqkv) {
     float csk[2] = {0.f, 0.f}, csv[2] = {0.f, 0.f};
-    qkv_sink32<bf16>(sink, 1, b, hh, H, k0, N, lane, dk, LN2, csk);
+    qkv_sink32<bf16>(sink, 1, b, hh, H, k0, N, lane, dk, -LN2, csk);
     qkv_sink32<bf16>(sink, 2, b, hh, H, k0, N, lane, dv, 1.f, csv);
     if (sink.ws) qkv_colsum32(sink, 2, hh, H, (blockIdx.y * gridDim.x + blockIdx.x) % S3OD_NREP, lane, csv);
     return;
@@ -975,27 +1024,29 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __r
     bf16* dvr = dV + ((long)bh * N + key) * 64;
 #pragma unroll
     for (int db = 0; db < 2; db++) {
-      dkr[32 * db + (lane & 31)] = (bf16)(dk[db][i] * LN2);
+      dkr[32 * db + (lane & 31)] = (bf16)(dk[db][i] * -LN2);
       dvr[32 * db + (lane & 31)] = (bf16)dv[db][i];
     }
   }
 }
 
-// dQ (w.r.t. the pre-scaled q).  Workgroup = W waves x 32 queries; loop over 64-key tiles.
-template <int W>
+// dQ (w.r.t. the pre-scaled q).  Workgroup = W waves x 32 queries; loop over 64-key tiles (K, V by LDS-DMA).
+// Same sign convention: Q and dO fragments negated, C = +LSE / +delta of the lane's query (constant blocks).
+template <int W, bool PRIO, bool IL>
 __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                                  const bf16* __restrict__ V, const bf16* __restrict__ dO,
                                                                  const float* __restrict__ LSE, const float* __restrict__ Dl,
                                                                  bf16* __restrict__ dQ, int N, int H, QkvSink sink) {
-  constexpr int NT = 64 * W, SB = 2 * Img32::BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[2 * SB];
+  constexpr int SB = 2 * Img32::BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * SB];
   const int bh = blockIdx.y, b = bh / H, hh = bh - b * H;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const bf16* Kp = K + (long)bh * N * 64;
-  const bf16* Vp = V + (long)bh * N * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5;
+  const auto rk = attn_rsrc(K + (long)bh * N * 64, (unsigned long)N * 128);
+  const auto rv = attn_rsrc(V + (long)bh * N * 64, (unsigned long)N * 128);
   const int q0 = blockIdx.x * (32 * W) + wave * 32;
+  if (PRIO && wave >= W / 2) __builtin_amdgcn_s_setprio(1);
   bf16x8 qf[4], of[4];
-  f32x16 nl, nd;     // C operands: -LSE (log2 units) / -delta of the lane's query, all 16 rows
+  f32x16 cl, cd;     // C operands: LSE (log2 units) / delta of the lane's query, all 16 rows
   {
     const int q = q0 + (lane & 31);
     const bf16* qr = Q + ((long)bh * N + q) * 64 + 8 * h;
@@ -1003,65 +1054,84 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __res
     bf16x8 z; for (int e = 0; e < 8; e++) z[e] = (bf16)0.f;
 #pragma unroll
     for (int ks = 0; ks < 4; ks++) {
-      qf[ks] = q < N ? *(const bf16x8*)(qr + 16 * ks) : z;
-      of[ks] = q < N ? *(const bf16x8*)(orow + 16 * ks) : z;
+      qf[ks] = q < N ? neg8(*(const bf16x8*)(qr + 16 * ks)) : z;
+      of[ks] = q < N ? neg8(*(const bf16x8*)(orow + 16 * ks)) : z;
     }
-    const float l = q < N ? -LSE[(long)bh * N + q] : -INFINITY, d = q < N ? -Dl[(long)bh * N + q] : 0.f;
+    const float l = q < N ? LSE[(long)bh * N + q] : INFINITY, d = q < N ? Dl[(long)bh * N + q] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; i++) { nl[i] = l; nd[i] = d; }
+    for (int i = 0; i < 16; i++) { cl[i] = l; cd[i] = d; }
   }
   f32x16 dq[2];
 #pragma unroll
   for (int db = 0; db < 2; db++) for (int i = 0; i < 16; i++) dq[db][i] = 0.f;
-  RowTile32<NT> tk, tv;
   const int nkt = (N + 63) / 64;
-  tk.load(Kp, 64, 0, N, tid); tv.load(Vp, 64, 0, N, tid);
-  tk.store(smem, tid); tv.store(smem + Img32::BYTES, tid);
+  auto stage = [&](int kt, char* base) {
+    Dma64<W>::issue(rk, (long)kt * 64, 128, base, wave, lane);
+    Dma64<W>::issue(rv, (long)kt * 64, 128, base + Img32::BYTES, wave, lane);
+  };
+  stage(0, smem);
   __syncthreads();
   int cur = 0;
   for (int kt = 0; kt < nkt; kt++) {
-    const bool more = kt + 1 < nkt;
-    if (more) { tk.load(Kp, 64, (kt + 1) * 64, N, tid); tv.load(Vp, 64, (kt + 1) * 64, N, tid); }
+    if (kt + 1 < nkt) stage(kt + 1, smem + (cur ^ 1) * SB);
     const char* ks_ = smem + cur * SB;
     const char* vs_ = ks_ + Img32::BYTES;
     f32x16 s[2], dp[2];
+    bf16x8 da[2][2];
+    auto sdp = [&](int kb) {
+      bf16x8 a[4], c[4];
 #pragma unroll
-    for (int kb = 0; kb < 2; kb++) {
-      s[kb] = mma32(row32(ks_, 32 * kb, 0, lane), qf[0], nl);
-      dp[kb] = mma32(row32(vs_, 32 * kb, 0, lane), of[0], nd);
+      for (int ks = 0; ks < 4; ks++) { a[ks] = row32(ks_, 32 * kb, ks, lane); c[ks] = row32(vs_, 32 * kb, ks, lane); }
+      s[kb] = mma32(a[0], qf[0], cl);
+      dp[kb] = mma32(c[0], of[0], cd);
 #pragma unroll
-      for (int ks = 1; ks < 4; ks++) {
-        s[kb] = mma32(row32(ks_, 32 * kb, ks, lane), qf[ks], s[kb]);
-        dp[kb] = mma32(row32(vs_, 32 * kb, ks, lane), of[ks], dp[kb]);
-      }
-    }
-    // dS^T = exp2(s - lse) * (dp - delta)
+      for (int ks = 1; ks < 4; ks++) { s[kb] = mma32(a[ks], qf[ks], s[kb]); dp[kb] = mma32(c[ks], of[ks], dp[kb]); }
+    };
+    // s = LSE - S^T, dp = delta - dP^T:  -dS^T = exp2(-s) * dp, packed as the A operand of dQ
+    auto softmax = [&](int kb) {
 #pragma unroll
-    for (int kb = 0; kb < 2; kb++)
-#pragma unroll
-      for (int i = 0; i < 16; i++) dp[kb][i] *= fexp2(s[kb][i]);
-    if (kt * 64 + 64 > N) {   // last tile: zero dS of keys >= N (exp2(-lse) may overflow)
-#pragma unroll
-      for (int kb = 0; kb < 2; kb++)
+      for (int i = 0; i < 16; i++) dp[kb][i] *= fexp2(-s[kb][i]);
+      if (kt * 64 + 64 > N) {   // last tile: zero dS of keys >= N (exp2(-lse) may overflow)
 #pragma unroll
         for (int i = 0; i < 16; i++)
           if (kt * 64 + 32 * kb + acc_row(i, h) >= N) dp[kb][i] = 0.f;
-    }
+      }
 #pragma unroll
-    for (int kb = 0; kb < 2; kb++)
+      for (int st = 0; st < 2; st++) da[kb][st] = pack_acc(dp[kb], st);
+    };
+    auto dqk = [&](int kb) {
 #pragma unroll
       for (int st = 0; st < 2; st++) {
-        const bf16x8 da = pack_acc(dp[kb], st);
+        bf16x8 bk[2];
 #pragma unroll
-        for (int db = 0; db < 2; db++) dq[db] = mma32(da, tr32(ks_, 32 * kb + 16 * st, 32 * db, lane), dq[db]);
+        for (int db = 0; db < 2; db++) bk[db] = tr32(ks_, 32 * kb + 16 * st, 32 * db, lane);
+#pragma unroll
+        for (int db = 0; db < 2; db++) dq[db] = mma32(da[kb][st], bk[db], dq[db]);
       }
-    if (more) { tk.store(smem + (cur ^ 1) * SB, tid); tv.store(smem + (cur ^ 1) * SB + Img32::BYTES, tid); }
+    };
+    auto interleave = [&](int n) {
+      for (int g = 0; g < n; g++) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+      }
+    };
+    sdp(0);
+    __builtin_amdgcn_sched_barrier(0);
+    sdp(1);
+    softmax(0);
+    if (IL) interleave(8);
+    __builtin_amdgcn_sched_barrier(0);
+    dqk(0);
+    softmax(1);
+    if (IL) interleave(4);
+    __builtin_amdgcn_sched_barrier(0);
+    dqk(1);
     __syncthreads();
     cur ^= 1;
   }
   if (sink.dqkv) {
     float csq[2] = {0.f, 0.f};
-    qkv_sink32<bf16>(sink, 0, b, hh, H, q0, N, lane, dq, 0.125f, csq);
+    qkv_sink32<bf16>(sink, 0, b, hh, H, q0, N, lane, dq, -0.125f, csq);
     if (sink.ws) qkv_colsum32(sink, 0, hh, H, (blockIdx.y * gridDim.x + blockIdx.x) % S3OD_NREP, lane, csq);
     return;
   }
@@ -1071,7 +1141,7 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __res
     if (q >= N) continue;
     bf16* r = dQ + ((long)bh * N + q) * 64;
 #pragma unroll
-    for (int db = 0; db < 2; db++) r[32 * db + (lane & 31)] = (bf16)dq[db][i];
+    for (int db = 0; db < 2; db++) r[32 * db + (lane & 31)] = (bf16)(-dq[db][i]);
   }
 }
 
@@ -1111,11 +1181,30 @@ void launch_bwd(const void* q, const void* k, const void* v, const void* o, cons
   hipLaunchKernelGGL(attn_delta_kernel<T>, dim3(cdiv((long)B * H * N * 8, 256)), dim3(256), 0, st, (const T*)o, (const T*)dout, delta, N, H, B * H);
   if constexpr (std::is_same<T, bf16>::value) {
     if (attn_bwd_variant() == 1) {
-      constexpr int W = 4;
-      hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<W>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st, (const bf16*)q, (const bf16*)k,
-                         (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv, N, H, sink);
-      hipLaunchKernelGGL((attn_bwd_dq32_kernel<W>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st, (const bf16*)q, (const bf16*)k,
-                         (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, N, H, sink);
+      // waves per workgroup (dev knobs for A/B: S3OD_ATTN_WK for the dK/dV pass, S3OD_ATTN_WQ for the dQ pass)
+      static const int wk = dev_knob("S3OD_ATTN_WK", 4), wq = dev_knob("S3OD_ATTN_WQ", 4), pr = dev_knob("S3OD_ATTN_PRIO", 0),
+                            il = dev_knob("S3OD_ATTN_IL", 0);
+      auto go_kv = [&](auto w) {
+        constexpr int W = decltype(w)::value;
+        if (pr) hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<W, true, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st, (const bf16*)q,
+                                   (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv, N, H, sink);
+        else if (il) hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<W, false, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st,
+                                        (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv,
+                                        N, H, sink);
+        else hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<W, false, false>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st, (const bf16*)q,
+                           (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv, N, H, sink);
+      };
+      auto go_q = [&](auto w) {
+        constexpr int W = decltype(w)::value;
+        if (pr) hipLaunchKernelGGL((attn_bwd_dq32_kernel<W, true, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st, (const bf16*)q,
+                                   (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, N, H, sink);
+        else if (il) hipLaunchKernelGGL((attn_bwd_dq32_kernel<W, false, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st,
+                                        (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, N, H, sink);
+        else hipLaunchKernelGGL((attn_bwd_dq32_kernel<W, false, false>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st, (const bf16*)q,
+                           (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, N, H, sink);
+      };
+      if (wk == 8) go_kv(std::integral_constant<int, 8>{}); else go_kv(std::integral_constant<int, 4>{});
+      if (wq == 8) go_q(std::integral_constant<int, 8>{}); else go_q(std::integral_constant<int, 4>{});
       return;
     }
   }

@@ -29,7 +29,7 @@ def timeit(fn, n=10):
 
 def main(out_path):
     res = {}
-    tag = f"bwd={os.environ.get('S3OD_ATTN_BWD', '32')}"
+    tag = f"bwd={os.environ.get('S3OD_ATTN_BWD', '32')} wk={os.environ.get('S3OD_ATTN_WK', '4')} wq={os.environ.get('S3OD_ATTN_WQ', '4')} prio={os.environ.get('S3OD_ATTN_PRIO', '0')} il={os.environ.get('S3OD_ATTN_IL', '0')}"
     for B, N in ((16, 4101), (4, 16389)):
         H = 12
         g = torch.Generator(device="cuda").manual_seed(B * N)
