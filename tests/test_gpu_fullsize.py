@@ -183,3 +183,69 @@ def test_c5_one_image_strict_vs_oracle(model):
     print(f"C5 strict vs oracle @2048: logits {e_m:.3g}, iou {e_i:.3g}")
     assert e_m <= 2e-4 and e_i <= 2e-4
     assert int(out["pred_iou"].argmax(1)) == int(ref["pred_iou"].argmax(1))
+
+
+# ------------------------------------------------------------------------------------ bf16 vs the oracle
+def test_bf16_vs_oracle_production_sizes(model):
+    """The bf16 fast path checked against the ORACLE (not against the build's own f32 path) at the sizes the
+    metric is quoted on: image 0 of a bs-8 1024^2 batch (C2) and of a bs-4 2048^2 batch (C5), and a bs-1
+    1024^2 train step's gradients (C3).  Reported with the flip band of SURVEY §8(c) (pixels whose oracle
+    logit lies within 2*max|d| of zero); written to gpurun_out/bf16_vs_oracle.json when that directory exists.
+    Bounds: logits rel-L2 <= 3e-2, sign agreement >= 0.98, every pixel outside the flip band agrees,
+    pred_iou rel-L2 <= 3e-2; C3 loss within 2 %, per-parameter gradient cosine >= 0.99."""
+    import json
+    import os
+    from oracle import s3od_oracle as O
+    from s3od_amd.model import DPTSegmentation
+    rec = {}
+    sd = _oracle_sd()
+    for tag, B, S, seed in (("C2", 8, 1024, 61), ("C5", 4, 2048, 62)):
+        x, _ = _batch(B, S, seed)
+        model.compute_dtype = "bf16"
+        with torch.no_grad():
+            out = model(x)
+            pm, iou = out["pred_masks"][:1].float().clone(), out["pred_iou"][:1].clone()
+            del out
+            ref = O.forward(x[:1].contiguous(), sd)
+        model.compute_dtype = "f32"
+        r = ref["pred_masks"]
+        d = (pm - r).abs()
+        maxd = float(d.max())
+        band = (r.abs() < 2 * maxd)
+        agree = ((pm > 0) == (r > 0))
+        inter = float(((pm > 0) & (r > 0)).sum()); union = float(((pm > 0) | (r > 0)).sum())
+        top2 = torch.topk(ref["pred_iou"][0], 2).values
+        rec[tag] = {"batch": B, "size": S, "logits_rel_l2": rel_l2(pm, r), "max_abs_diff": maxd,
+                    "median_abs_logit": float(r.abs().median()), "flip_band_fraction": float(band.float().mean()),
+                    "sign_agreement": float(agree.float().mean()), "sign_agreement_outside_band": float(agree[~band].float().mean()),
+                    "mask_iou": inter / max(union, 1.0), "pred_iou_rel_l2": rel_l2(iou, ref["pred_iou"]),
+                    "best_idx": int(iou.argmax(1)), "best_idx_ref": int(ref["pred_iou"].argmax(1)),
+                    "ref_top2_margin": float(top2[0] - top2[1])}
+        del ref, pm, r, d, band, agree, x
+        torch.cuda.empty_cache()
+    # C3: one train step at bs 1, 1024^2, bf16 vs the oracle's autograd
+    x, masks = _batch(1, 1024, 63)
+    m = DPTSegmentation(compute_dtype="bf16").cuda()
+    loss, _, grads = _train_grads(m, x, masks)
+    del m
+    sdg = _oracle_sd(requires_grad=True)
+    ref = O.forward(x, sdg, train=True, rope_rescale=1.3)
+    rloss, *_ = O.multi_mask_loss(ref, masks, 0)
+    rloss.backward()
+    cos = sorted((cosine(g, sdg[n].grad), n) for n, g in grads.items()
+                 if not ("resConfUnit" in n and (n.endswith("conv1.bias") or n.endswith("conv2.bias"))))
+    rec["C3"] = {"batch": 1, "size": 1024, "loss": loss, "loss_ref": float(rloss),
+                 "worst_grad_cosine": cos[0][0], "worst_param": cos[0][1],
+                 "median_grad_cosine": cos[len(cos) // 2][0]}
+    print("bf16 vs oracle:", json.dumps(rec))
+    if os.path.isdir("gpurun_out"):
+        json.dump(rec, open("gpurun_out/bf16_vs_oracle.json", "w"), indent=1)
+    for tag in ("C2", "C5"):
+        r = rec[tag]
+        assert r["logits_rel_l2"] <= 3e-2 and r["sign_agreement"] >= 0.98, (tag, r)
+        assert r["sign_agreement_outside_band"] == 1.0, (tag, r)
+        assert r["pred_iou_rel_l2"] <= 3e-2, (tag, r)
+        if r["ref_top2_margin"] > 0.05:
+            assert r["best_idx"] == r["best_idx_ref"], (tag, r)
+    assert abs(rec["C3"]["loss"] - rec["C3"]["loss_ref"]) <= 2e-2 * abs(rec["C3"]["loss_ref"])
+    assert rec["C3"]["worst_grad_cosine"] >= 0.99, rec["C3"]
