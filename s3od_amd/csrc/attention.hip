@@ -1269,9 +1269,10 @@ extern "C" {
 // q,k,v: [B*H, N, 64] (q pre-scaled by log2(e)/8); o: [B, N, H*64]; lse: [B*H, N] fp32, log2 units (optional)
 int s3od_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int N, void* stream) {
   dim3 grid(cdiv(N, 128), B * H);
-  // bf16: the 32x32x16 kernel (S3OD_ATTN_FWD=16 selects the 16x16x32 one, for A/B measurement)
-  static const int fwd16 = dev_knob("S3OD_ATTN_FWD", 32) == 16;
-  if (dtype == S3OD_BF16 && !fwd16) {
+  // bf16: the 16x16x32 kernel; the 32x32x16 one (S3OD_ATTN_FWD=32) measured 6-8 % slower (1083 -> 1150 us at
+  // bs 16, N 4101; 3532 -> 3817 us at bs 4, N 16389, same box): its extra row-sum MFMAs cost 2x the cycles
+  static const int fwd32 = dev_knob("S3OD_ATTN_FWD", 16) == 32;
+  if (dtype == S3OD_BF16 && fwd32) {
     hipLaunchKernelGGL((attn_fwd32_kernel<4>), grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)q, (const bf16*)k,
                        (const bf16*)v, (bf16*)o, lse, N, H);
     return s3od_check_launch("attn_fwd");
