@@ -884,7 +884,31 @@ template <int W> struct Dma64 {
     }
   }
 };
+// The same with the descriptor rebased on the tile's first row (scalar work only): the per-lane source offsets are
+// loop-invariant registers, so a tile's DMA issue costs no vector ALU.  `total` = the buffer's byte size from `base`;
+// rows past its end still read zeros (range check against the rebased size).
+template <int W> struct Dma64R {
+  static constexpr int NIW = 8 / W;
+  unsigned vo[NIW];
+  DEV void init(long ldb, int wave, int lane) {
+#pragma unroll
+    for (int i = 0; i < NIW; i++) {
+      const int o = (wave * NIW + i) * 1024 + lane * 16, row = o >> 7, lc = ((o >> 4) & 7) ^ Img32::sw(row);
+      vo[i] = (unsigned)(row * ldb + lc * 16);
+    }
+  }
+  DEV void issue(const char* base, unsigned long total, long row0, long ldb, char* img, int wave) const {
+    const long off = row0 * ldb;
+    const auto r = attn_rsrc(base + off, total - off);
+#pragma unroll
+    for (int i = 0; i < NIW; i++)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(img + (wave * NIW + i) * 1024), 16, vo[i], 0, 0, 0);
+  }
+};
 // 64 fp32 row constants (LSE or delta of one 64-query tile) by one wave's LDS-DMA (lanes 0..15 carry data)
+DEV void dma_row64r(const float* base, int N, int q0, unsigned vo, char* dst) {   // vo = lane < 16 ? 16 lane : OOB
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(attn_rsrc(base + q0, (unsigned long)(N - q0) * 4), (lds_void*)dst, 16, vo, 0, 0, 0);
+}
 DEV void dma_row64(__amdgpu_buffer_rsrc_t r, long q0, char* dst, int lane) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, lane < 16 ? (unsigned)((q0 + 4 * lane) * 4) : 0x80000000u, 0, 0, 0);
 }
@@ -906,7 +930,7 @@ DEV bf16x8 neg8(bf16x8 v) {
 // flipped at the store.
 // PRIO: the second half of the workgroup's waves run at s_setprio 1 (MI355X_MICROARCH "Two waves per SIMD" item 4)
 // IL: interleave the softmax VALU of one 32-query half between the other half's MFMAs (sched_group_barrier)
-template <int W, bool PRIO, bool IL>
+template <int W, bool PRIO, bool IL, bool U2 = false>
 __global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                                    const bf16* __restrict__ V, const bf16* __restrict__ dO,
                                                                    const float* __restrict__ LSE, const float* __restrict__ Dl,
@@ -921,6 +945,9 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __r
   const auto rdo = attn_rsrc(dO + (long)b * N * ldo + hh * 64, ((unsigned long)(N - 1) * ldo + 64) * 2);
   const auto rl = attn_rsrc(LSE + (long)bh * N, (unsigned long)N * 4);
   const auto rd = attn_rsrc(Dl + (long)bh * N, (unsigned long)N * 4);
+  Dma64R<W> dq_, ddo;
+  if constexpr (U2) { dq_.init(128, wave, lane); ddo.init(ldo * 2, wave, lane); }
+  const unsigned vrow = lane < 16 ? 16u * lane : 0x80000000u;
   const int k0 = blockIdx.x * (32 * W) + wave * 32;
   if (PRIO && wave >= W / 2) __builtin_amdgcn_s_setprio(1);
   bf16x8 kf[4], vf[4];
@@ -940,15 +967,25 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __r
   for (int db = 0; db < 2; db++) for (int i = 0; i < 16; i++) { dk[db][i] = 0.f; dv[db][i] = 0.f; }
   const int nqt = (N + 63) / 64;
   auto stage = [&](int qt, char* base) {
-    Dma64<W>::issue(rq, (long)qt * 64, 128, base, wave, lane);
-    Dma64<W>::issue(rdo, (long)qt * 64, ldo * 2, base + Img32::BYTES, wave, lane);
-    if (wave == 0) dma_row64(rl, (long)qt * 64, base + 2 * Img32::BYTES, lane);
-    if (wave == W - 1) dma_row64(rd, (long)qt * 64, base + 2 * Img32::BYTES + 1024, lane);
+    if constexpr (U2) {
+      dq_.issue((const char*)(Q + (long)bh * N * 64), (unsigned long)N * 128, (long)qt * 64, 128, base, wave);
+      ddo.issue((const char*)(dO + (long)b * N * ldo + hh * 64), ((unsigned long)(N - 1) * ldo + 64) * 2, (long)qt * 64, ldo * 2,
+                base + Img32::BYTES, wave);
+      if (wave == 0) dma_row64r(LSE + (long)bh * N, N, qt * 64, vrow, base + 2 * Img32::BYTES);
+      if (wave == W - 1) dma_row64r(Dl + (long)bh * N, N, qt * 64, vrow, base + 2 * Img32::BYTES + 1024);
+    } else {
+      Dma64<W>::issue(rq, (long)qt * 64, 128, base, wave, lane);
+      Dma64<W>::issue(rdo, (long)qt * 64, ldo * 2, base + Img32::BYTES, wave, lane);
+      if (wave == 0) dma_row64(rl, (long)qt * 64, base + 2 * Img32::BYTES, lane);
+      if (wave == W - 1) dma_row64(rd, (long)qt * 64, base + 2 * Img32::BYTES + 1024, lane);
+    }
   };
   stage(0, smem);
   __syncthreads();
-  int cur = 0;
-  for (int qt = 0; qt < nqt; qt++) {
+  // U2: the tile loop unrolled by two so the LDS stage is a compile-time constant (every fragment address
+  // becomes a per-lane base + immediate instead of being recomputed from the stage index each tile)
+  auto tile = [&](int qt, auto CUR) {
+    const int cur = CUR;     // std::integral_constant (U2) or the runtime stage index
     if (qt + 1 < nqt) stage(qt + 1, smem + (cur ^ 1) * SB);
     const char* qs_ = smem + cur * SB;
     const char* dos = qs_ + Img32::BYTES;
@@ -1007,7 +1044,14 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __r
     __builtin_amdgcn_sched_barrier(0);
     dvdk(1);
     __syncthreads();      // drains this tile's reads and the next tile's LDS-DMA (vmcnt(0)) before the flip
-    cur ^= 1;
+  };
+  if constexpr (U2) {
+    int qt = 0;
+    for (; qt + 1 < nqt; qt += 2) { tile(qt, std::integral_constant<int, 0>{}); tile(qt + 1, std::integral_constant<int, 1>{}); }
+    if (qt < nqt) tile(qt, std::integral_constant<int, 0>{});
+  } else {
+    int cur = 0;
+    for (int qt = 0; qt < nqt; qt++) { tile(qt, cur); cur ^= 1; }
   }
   if (sink.dqkv) {
     float csk[2] = {0.f, 0.f}, csv[2] = {0.f, 0.f};
@@ -1032,7 +1076,7 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __r
 
 // dQ (w.r.t. the pre-scaled q).  Workgroup = W waves x 32 queries; loop over 64-key tiles (K, V by LDS-DMA).
 // Same sign convention: Q and dO fragments negated, C = +LSE / +delta of the lane's query (constant blocks).
-template <int W, bool PRIO, bool IL>
+template <int W, bool PRIO, bool IL, bool U2 = false>
 __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                                  const bf16* __restrict__ V, const bf16* __restrict__ dO,
                                                                  const float* __restrict__ LSE, const float* __restrict__ Dl,
@@ -1043,6 +1087,8 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __res
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5;
   const auto rk = attn_rsrc(K + (long)bh * N * 64, (unsigned long)N * 128);
   const auto rv = attn_rsrc(V + (long)bh * N * 64, (unsigned long)N * 128);
+  Dma64R<W> dkv;
+  if constexpr (U2) dkv.init(128, wave, lane);
   const int q0 = blockIdx.x * (32 * W) + wave * 32;
   if (PRIO && wave >= W / 2) __builtin_amdgcn_s_setprio(1);
   bf16x8 qf[4], of[4];
@@ -1066,13 +1112,18 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __res
   for (int db = 0; db < 2; db++) for (int i = 0; i < 16; i++) dq[db][i] = 0.f;
   const int nkt = (N + 63) / 64;
   auto stage = [&](int kt, char* base) {
-    Dma64<W>::issue(rk, (long)kt * 64, 128, base, wave, lane);
-    Dma64<W>::issue(rv, (long)kt * 64, 128, base + Img32::BYTES, wave, lane);
+    if constexpr (U2) {
+      dkv.issue((const char*)(K + (long)bh * N * 64), (unsigned long)N * 128, (long)kt * 64, 128, base, wave);
+      dkv.issue((const char*)(V + (long)bh * N * 64), (unsigned long)N * 128, (long)kt * 64, 128, base + Img32::BYTES, wave);
+    } else {
+      Dma64<W>::issue(rk, (long)kt * 64, 128, base, wave, lane);
+      Dma64<W>::issue(rv, (long)kt * 64, 128, base + Img32::BYTES, wave, lane);
+    }
   };
   stage(0, smem);
   __syncthreads();
-  int cur = 0;
-  for (int kt = 0; kt < nkt; kt++) {
+  auto tile = [&](int kt, auto CUR) {      // U2: as in the dK/dV pass
+    const int cur = CUR;
     if (kt + 1 < nkt) stage(kt + 1, smem + (cur ^ 1) * SB);
     const char* ks_ = smem + cur * SB;
     const char* vs_ = ks_ + Img32::BYTES;
@@ -1127,7 +1178,14 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __res
     __builtin_amdgcn_sched_barrier(0);
     dqk(1);
     __syncthreads();
-    cur ^= 1;
+  };
+  if constexpr (U2) {
+    int kt = 0;
+    for (; kt + 1 < nkt; kt += 2) { tile(kt, std::integral_constant<int, 0>{}); tile(kt + 1, std::integral_constant<int, 1>{}); }
+    if (kt < nkt) tile(kt, std::integral_constant<int, 0>{});
+  } else {
+    int cur = 0;
+    for (int kt = 0; kt < nkt; kt++) { tile(kt, cur); cur ^= 1; }
   }
   if (sink.dqkv) {
     float csq[2] = {0.f, 0.f};
@@ -1144,6 +1202,16 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __res
     for (int db = 0; db < 2; db++) r[32 * db + (lane & 31)] = (bf16)(-dq[db][i]);
   }
 }
+
+// (hipcc 7.2 left the host stubs of these instances undefined when they were only named in the launcher below)
+template __global__ void attn_bwd_dq32_kernel<4, false, false, true>(const bf16*, const bf16*, const bf16*, const bf16*, const float*,
+                                                                     const float*, bf16*, int, int, QkvSink);
+template __global__ void attn_bwd_dq32_kernel<8, false, false, true>(const bf16*, const bf16*, const bf16*, const bf16*, const float*,
+                                                                     const float*, bf16*, int, int, QkvSink);
+template __global__ void attn_bwd_dkdv32_kernel<4, false, false, true>(const bf16*, const bf16*, const bf16*, const bf16*, const float*,
+                                                                       const float*, bf16*, bf16*, int, int, QkvSink);
+template __global__ void attn_bwd_dkdv32_kernel<8, false, false, true>(const bf16*, const bf16*, const bf16*, const bf16*, const float*,
+                                                                       const float*, bf16*, bf16*, int, int, QkvSink);
 
 // ===================================================================================== forward, bf16, 32x32x16
 // Same algorithm as attn_fwd_kernel (swapped products, lazy rescale with the running max in the S MFMA's C
@@ -1310,10 +1378,13 @@ void launch_bwd(const void* q, const void* k, const void* v, const void* o, cons
     if (attn_bwd_variant() == 1) {
       // waves per workgroup (dev knobs for A/B: S3OD_ATTN_WK for the dK/dV pass, S3OD_ATTN_WQ for the dQ pass)
       static const int wk = dev_knob("S3OD_ATTN_WK", 4), wq = dev_knob("S3OD_ATTN_WQ", 4), pr = dev_knob("S3OD_ATTN_PRIO", 0),
-                            il = dev_knob("S3OD_ATTN_IL", 0);
+                            il = dev_knob("S3OD_ATTN_IL", 0), u2 = dev_knob("S3OD_ATTN_U2", 1);
       auto go_kv = [&](auto w) {
         constexpr int W = decltype(w)::value;
-        if (pr) hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<W, true, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st, (const bf16*)q,
+        if (u2) hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<W, false, false, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st,
+                                   (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv,
+                                   N, H, sink);
+        else if (pr) hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<W, true, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st, (const bf16*)q,
                                    (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv, N, H, sink);
         else if (il) hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<W, false, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st,
                                         (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv,
@@ -1323,7 +1394,9 @@ void launch_bwd(const void* q, const void* k, const void* v, const void* o, cons
       };
       auto go_q = [&](auto w) {
         constexpr int W = decltype(w)::value;
-        if (pr) hipLaunchKernelGGL((attn_bwd_dq32_kernel<W, true, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st, (const bf16*)q,
+        if (u2) hipLaunchKernelGGL((attn_bwd_dq32_kernel<W, false, false, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st,
+                                   (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, N, H, sink);
+        else if (pr) hipLaunchKernelGGL((attn_bwd_dq32_kernel<W, true, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st, (const bf16*)q,
                                    (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, N, H, sink);
         else if (il) hipLaunchKernelGGL((attn_bwd_dq32_kernel<W, false, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st,
                                         (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, N, H, sink);
