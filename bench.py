@@ -17,6 +17,8 @@ entry timed, plus the whole-step MFMA fraction and the ViT-encoder ("attention b
 host's cores (rank 0, N=1 only): 1 warm-up + --cpu-iters (3) timed iterations of one image (BASELINE.md
 "CPU-baseline plan": 1 + >= 3), for the train step and for C2 (the `infer` object); the C5 baseline in
 `infer_2048` is one timed 2048^2 image without warm-up (~80 s of CPU per image on the box's share).
+`c1`: configs[0], `BackgroundRemoval.remove_background` on the reference's fixture image end to end (host
+image in, RemovalResult out) beside the oracle's CPU restatement of the same pipeline (1 + 2 iterations).
 Attention backward work follows SURVEY §8(d) (8*N^2*64 per (b,h), recompute not counted); the roofline
 object also carries the executed figure (14*N^2*64) for that entry.
 """
@@ -236,6 +238,63 @@ def infer_rate(model, B, S, steps, warmup, dev, cpu_iters):
     return res
 
 
+def c1_plumbing(dev, cpu_iters, steps=10, warmup=2):
+    """configs[0]: BackgroundRemoval.remove_background on the reference's fixture image end to end (PIL image in ->
+    RemovalResult out: upload, device letterbox + normalise, eval forward, sigmoid/unpad/antialias resize, the masks'
+    copy back, RGBA compose), synthetic weights.  Host round trips included, so this is a plumbing figure, not `value`.
+    CPU leg: the oracle's restatement of the same pipeline (oracle/s3od_oracle.py get_pad_info / normalize / forward /
+    postprocess = predictor.py:96-139), 1 warm-up + `cpu_iters` timed."""
+    from PIL import Image
+    from s3od_amd.predictor import BackgroundRemoval
+    img = Image.open(Path(__file__).resolve().parent / "tests" / "fixture" / "image.jpg").convert("RGB")
+    log(f"C1 remove_background on the fixture ({img.size[0]}x{img.size[1]})")
+    br = BackgroundRemoval("synthetic", device=str(dev))
+    for _ in range(warmup):
+        br.remove_background(img)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res = br.remove_background(img)
+    dt = (time.perf_counter() - t0) / steps
+    out = {"value": round(1.0 / dt, 3), "unit": "images/s", "ms_per_call": round(dt * 1e3, 3), "calls": steps,
+           "warmup": warmup, "image": f"tests/fixture/image.jpg {img.size[0]}x{img.size[1]}", "dtype": "bf16",
+           "best_idx": int(res.all_ious.argmax()),
+           "config": "configs[0]: BackgroundRemoval.remove_background(fixture) end to end, host image in / masks out"}
+    del br
+    if cpu_iters > 0:
+        try:
+            import numpy as np
+            from oracle import s3od_oracle as O
+            from s3od_amd.weights import synthetic_state_dict
+            threads = cpu_threads()
+            torch.set_num_threads(threads)
+            sd = {k: torch.from_numpy(v) for k, v in synthetic_state_dict(0).items()}
+            arr = np.array(img)
+
+            def run():
+                pad = O.get_pad_info(arr.shape[0], arr.shape[1], 1024)
+                assert pad["resized_size"] == arr.shape[:2], "fixture is 1024^2: no resize step"
+                x = O.normalize(arr)
+                with torch.no_grad():
+                    o = O.forward(x, sd)
+                return O.postprocess(o["pred_masks"], o["pred_iou"], pad)
+            run()
+            ts = []
+            for it in range(cpu_iters):
+                t1 = time.perf_counter()
+                run()
+                ts.append(time.perf_counter() - t1)
+                log(f"cpu baseline C1: iteration {it + 1}/{cpu_iters} {ts[-1]:.2f} s")
+            ct = sum(ts) / len(ts)
+            out["cpu_baseline"] = {"value": round(1.0 / ct, 5), "unit": "images/s", "cores": threads, "kind": "port",
+                                   "iter_s": [round(t, 3) for t in ts],
+                                   "sample": f"the fixture through the oracle's remove_background pieces (fp32), 1 warm-up + "
+                                             f"{cpu_iters} timed, {threads} threads"}
+        except Exception as e:  # reported, never fatal for the GPU number
+            out["cpu_baseline"] = {"value": None, "error": repr(e)[:200]}
+    return out
+
+
 # ------------------------------------------------------------------------------------ launcher
 def _free_port():
     s = socket.socket()
@@ -424,6 +483,10 @@ def main():
                                 config="dinob inference bs=8 1024x1024 eval forward (configs[1])")
             res["infer_2048"] = dict(infer_rate(model, 4, 2048, 4, 2, dev, ci),
                                      config="high-res 2048x2048 eval forward bs=4 (configs[4])")
+            try:
+                res["c1"] = c1_plumbing(dev, min(ci, 2))
+            except Exception as e:  # reported, never fatal for the headline number
+                res["c1"] = {"value": None, "error": repr(e)[:200]}
         if not args.no_cpu_baseline and world == 1:
             try:
                 res["cpu_baseline"] = cpu_baseline(S, args.mode, args.cpu_iters)

@@ -320,6 +320,223 @@ static int launch_halo(const bf16* x, const bf16* w, EPI epi, int B, int H, int 
   return s3od_check_launch("conv3x3_halo");
 }
 
+// ---------------------------------------------------------------- register-weight 3x3 conv, 64 -> 64
+// The full-resolution 64-channel convs (upsample_2x.2 forward and its stride-1 data gradient) move
+// 4.3 / 6.4 GB per call at bs 16 (1024^2): HBM-bound at ~5.5 TB/s if loads, MFMAs and stores overlap.
+//   * one workgroup of 4 waves per CU (one wave per SIMD); wave w = output rows 4 (w>>1) .. +3 of the
+//     tile x output channels 32 (w&1) .. +31 and holds those channels' 9 taps x 64 weights as MFMA A
+//     fragments in registers (144 VGPRs), so the only LDS traffic is the input halo (B fragments);
+//   * tile = 8 x 32 output pixels; its (8+2) x (32+2) x 64 halo arrives by LDS-DMA (44 x 1 KiB pieces,
+//     11 per wave, zeros outside the image via the buffer range check) into a 3-deep ring, issued two
+//     tiles ahead, so the only per-tile synchronisation is one s_barrier behind a counted vmcnt;
+//   * the epilogue runs from the accumulators: bias / ReLU (forward) or the ReLU' mask of res1 (data
+//     gradient, its rows loaded at the start of the tile), the lane pair (lg, lg^1) trades 4-channel
+//     groups so every lane stores one 16-B run of 8 channels per 16-pixel block; column sums of the
+//     output (bias gradient) go through LDS atomics, one global flush per workgroup.
+constexpr int RW_TH = 8, RW_TW = 32, RW_HC = RW_TW + 2, RW_PX = (RW_TH + 2) * RW_HC;   // 340 halo pixels
+constexpr int RW_PIECES = 44, RW_PPW = RW_PIECES / 4;    // 1 KiB DMA pieces per halo (42.5 KiB + pad), per wave
+constexpr int RW_BUF = RW_PIECES * 1024, RW_LDS = 3 * RW_BUF;     // + 256 B of bias / column sums
+static_assert(RW_PX * 128 <= RW_BUF && RW_LDS + 256 <= 160 * 1024, "register-weight conv LDS budget");
+
+// MODE 0: out = acc + bias;  MODE 2: out = ReLU(acc + bias);  MODE 1: out = res1 > 0 ? acc : 0, colsum += out
+// Every wave issues a FIXED sequence of vector-memory instructions per tile (11 DMA pieces, 8 mask loads, 8 stores:
+// dummy pieces / out-of-image lanes use an out-of-range buffer offset instead of a branch), so the counted vmcnt
+// that retires a tile's halo is a per-phase constant.
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+template <int MODE>
+__global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                                 const float* __restrict__ bias,
+                                                                 const bf16* __restrict__ res1, float* __restrict__ colsum,
+                                                                 bf16* __restrict__ out, int H, int W, int tiles_x,
+                                                                 int tiles_y, int ntiles) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int lr = lane & 15, lg = lane >> 4, odd = lg & 1;
+  const int row0 = 4 * (wave >> 1), ch0 = 32 * (wave & 1);      // this wave's output rows / channels
+  // tiles: XCD x = blockIdx % 8 owns the contiguous range [x*n/8, (x+1)*n/8) (neighbouring tiles share halo
+  // rows in that XCD's L2); its workgroups stride through it
+  const int nwg = gridDim.x, xcd = blockIdx.x & 7, wpx = (nwg + 7 - xcd) >> 3, wi = blockIdx.x >> 3;
+  const int t_beg = (int)((long)ntiles * xcd / 8), t_end = (int)((long)ntiles * (xcd + 1) / 8);
+  const long img = (long)H * W * 64;                       // elements per image
+
+  // weights -> registers: lane (lr, lg) holds w[co = ch0 + 16 nb + lr][tap][ci = 32 kk + 8 lg .. +7]
+  bf16x8 wr[9][2][2];
+#pragma unroll
+  for (int tap = 0; tap < 9; tap++)
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+      for (int nb = 0; nb < 2; nb++)
+        wr[tap][kk][nb] = *(const bf16x8*)(w + ((long)(ch0 + nb * 16 + lr) * 9 + tap) * 64 + kk * 32 + lg * 8);
+
+  // DMA lane constants: piece p = 11 wave + i covers LDS bytes [1024 p, 1024 p + 1024) of a ring slot, laid out
+  // [px][16-B slot], slot = chunk ^ (px & 7); lane writes bytes 16 lane .. +15 of the piece
+  int dm[RW_PPW];
+#pragma unroll
+  for (int i = 0; i < RW_PPW; i++) {
+    const int b = (wave * RW_PPW + i) * 1024 + lane * 16, px = b >> 7, ch = ((b >> 4) & 7) ^ (px & 7);
+    dm[i] = px < RW_PX ? ((px / RW_HC) << 16) | ((px % RW_HC) << 4) | ch : -1;
+  }
+  auto issue = [&](int tile, int slot) {            // tile >= t_end: dummy pieces (zeros into a free slot)
+    const bool live = tile < t_end;
+    const int tc = live ? tile : t_beg;
+    const int txi = tc % tiles_x, t2 = tc / tiles_x, tyi = t2 % tiles_y, bb = t2 / tiles_y;
+    const int ty0 = tyi * RW_TH - 1, tx0 = txi * RW_TW - 1;
+    const auto r = make_rsrc(x + bb * img, (unsigned long)img * 2);
+    char* dst = smem + slot * RW_BUF + wave * RW_PPW * 1024;
+#pragma unroll
+    for (int i = 0; i < RW_PPW; i++) {
+      const int v = dm[i], gy = ty0 + (v >> 16), gx = tx0 + ((v >> 4) & 0xfff);
+      const bool ok = live && v >= 0 && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+      blds16(r, ok ? (unsigned)((gy * W + gx) * 128 + (v & 15) * 16) : 0x80000000u, dst + i * 1024);
+    }
+  };
+  // halo fragment addresses: px = L + off (L = row0 * 34 + lr per lane, off compile-time per (pb, tap)), byte
+  // px * 128 + (((4 kk + lg) ^ (px & 7)) << 4) = yb[(off & 7)][kk] + 128 off  (the XOR term depends on the lane
+  // and on off & 7 only), so every ds_read is a per-lane base + an immediate
+  int yb[8][2];
+  {
+    const int L = row0 * RW_HC + lr;
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+#pragma unroll
+      for (int kk = 0; kk < 2; kk++) yb[j][kk] = L * 128 + (((kk * 4 + lg) ^ ((L + j) & 7)) << 4);
+  }
+  // after the lane-pair trade in the epilogue a lane owns channels cb .. cb+7 of its pixel
+  const int cb = ch0 + (odd ? 16 : 0) + 8 * (lg >> 1);
+  // 64 floats after the ring: the bias (MODE 0, the accumulators' initial value) or the column sums (MODE 1)
+  float* aux = (float*)(smem + RW_LDS);
+  if (tid < 64) aux[tid] = (MODE != 1 && bias) ? bias[tid] : 0.f;
+  __syncthreads();
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
+  int tile = t_beg + wi, k = 0;
+  issue(tile, 0);
+  issue(tile + wpx, 1);
+  for (; tile < t_end; tile += wpx, k++) {
+    const int txi = tile % tiles_x, t2 = tile / tiles_x, tyi = t2 % tiles_y, bb = t2 / tiles_y;
+    const auto ro = make_rsrc(out + bb * img, (unsigned long)img * 2);
+    unsigned po[8];                                   // byte offset of this lane's 8-channel run per 16-px block (or OOB)
+#pragma unroll
+    for (int pb = 0; pb < 8; pb++) {
+      const int gy = tyi * RW_TH + row0 + (pb >> 1), gx = txi * RW_TW + (pb & 1) * 16 + lr;
+      po[pb] = (gy < H && gx < W) ? (unsigned)((gy * W + gx) * 128 + cb * 2) : 0x80000000u;
+    }
+    // data-gradient mask runs of this tile, issued before the next halo's DMA (their wait leaves it in flight)
+    u32x4v rm_[8];
+    if constexpr (MODE == 1) {
+      const auto rr = make_rsrc(res1 + bb * img, (unsigned long)img * 2);
+#pragma unroll
+      for (int pb = 0; pb < 8; pb++) rm_[pb] = __builtin_amdgcn_raw_buffer_load_b128(rr, po[pb], 0, 0);
+    }
+    // retire this tile's halo (own pieces): the vector-memory ops issued after them are a per-phase constant
+    //   k = 0: next halo (11) [+ masks 8];  k = 1: [masks 8,] halo 11, stores 8 [, masks 8];
+    //   k >= 2: stores 8 [, masks 8], halo 11, stores 8 [, masks 8]
+    if (k == 0) { if constexpr (MODE == 1) wait_vmcnt<RW_PPW + 8>(); else wait_vmcnt<RW_PPW>(); }
+    else if (k == 1) { if constexpr (MODE == 1) wait_vmcnt<8 + RW_PPW + 8 + 8>(); else wait_vmcnt<RW_PPW + 8>(); }
+    else { if constexpr (MODE == 1) wait_vmcnt<8 + 8 + RW_PPW + 8 + 8>(); else wait_vmcnt<8 + RW_PPW + 8>(); }
+    __builtin_amdgcn_s_barrier();                     // every wave's pieces landed; every wave done with slot k-1
+    asm volatile("" ::: "memory");
+    issue(tile + 2 * wpx, (k + 2) % 3);
+    const char* hb = smem + (k % 3) * RW_BUF;
+    f32x4 acc[8][2];                                  // acc[pb][nb]: D[co = ch0 + 16 nb + 4 lg + e][px = 16 pb + lr]
+#pragma unroll
+    for (int nb = 0; nb < 2; nb++) {
+      const f32x4 b0 = MODE != 1 ? *(const f32x4*)(aux + ch0 + nb * 16 + 4 * lg) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int pb = 0; pb < 8; pb++) acc[pb][nb] = b0;
+    }
+    // 18 (tap, k-half) steps of 16 MFMAs; the next step's 8 halo fragments are read before this step's MFMAs
+    auto rd = [&](int st, bf16x8 (&fa)[8]) {
+      const int tap = st >> 1, kk = st & 1, dy = tap / 3, dx = tap - 3 * (tap / 3);
+#pragma unroll
+      for (int pb = 0; pb < 8; pb++) {
+        const int off = ((pb >> 1) + dy) * RW_HC + (pb & 1) * 16 + dx;
+        fa[pb] = *(const bf16x8*)(hb + yb[off & 7][kk] + off * 128);
+      }
+    };
+    auto mm = [&](int st, const bf16x8 (&fa)[8]) {
+#pragma unroll
+      for (int pb = 0; pb < 8; pb++)
+#pragma unroll
+        for (int nb = 0; nb < 2; nb++)
+          acc[pb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[st >> 1][st & 1][nb], fa[pb], acc[pb][nb], 0, 0, 0);
+    };
+    bf16x8 fa0[8], fa1[8];
+    rd(0, fa0);
+#pragma unroll
+    for (int st = 0; st < 18; st += 2) {
+      rd(st + 1, fa1);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(st, fa0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (st + 2 < 18) rd(st + 2, fa0);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(st + 1, fa1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // epilogue: lane holds out[px = 16 pb + lr][co = ch0 + 16 nb + 4 lg .. +3]; the pair (lg, lg^1) trades
+    // so the even lane keeps nb 0 (channels cb .. cb+7) and the odd lane nb 1
+#pragma unroll
+    for (int pb = 0; pb < 8; pb++) {
+      // v_permlane16_swap: rows 1 / 3 of the first operand <-> rows 0 / 2 of the second (row = 16 lanes = one lg):
+      // even lg keeps its nb 0 and receives the odd partner's nb 0, the odd lg keeps nb 1 and receives the even's
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        float v0 = acc[pb][0][e], v1 = acc[pb][1][e];
+        if (MODE == 2) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); }
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(v0), __float_as_uint(v1), false, false);
+        o[e] = __uint_as_float(sw[0]);               // channels cb + 0..3
+        o[4 + e] = __uint_as_float(sw[1]);           // channels cb + 4..7
+      }
+      if constexpr (MODE == 1) {
+        const bf16x8 m = __builtin_bit_cast(bf16x8, rm_[pb]);
+#pragma unroll
+        for (int e = 0; e < 8; e++) o[e] = (float)m[e] > 0.f ? o[e] : 0.f;   // out-of-image lanes: mask reads 0
+#pragma unroll
+        for (int e = 0; e < 8; e++) cs[e] += o[e];     // column sums of channels cb .. cb+7 (lane partials)
+      }
+      bf16x8 ob;
+#pragma unroll
+      for (int e = 0; e < 8; e++) ob[e] = (bf16)o[e];
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, ob), ro, po[pb], 0, 0);
+    }
+  }
+  if (MODE == 1 && colsum) {                          // 16 lanes (lr) -> 1, LDS atomics, one global add per channel
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      float c = cs[e];
+      c += __shfl_xor(c, 1); c += __shfl_xor(c, 2); c += __shfl_xor(c, 4); c += __shfl_xor(c, 8);
+      if (lr == 0) atomicAdd(aux + cb + e, c);
+    }
+    __syncthreads();
+    if (tid < 64) atomicAdd(colsum + tid, aux[tid]);
+  }
+  wait_vmcnt<0>();        // no LDS-DMA (dummy pieces included) may still be landing when the workgroup retires
+}
+
+// S3OD_CONV_RW=0 disables the path (read per call: an A/B inside one process)
+static bool rw_ok(int dtype, int B, int H, int W) {
+  const char* e = getenv("S3OD_CONV_RW");
+  return dtype == S3OD_BF16 && !(e && atoi(e) == 0) && (long)H * W * 128 < (1L << 31) && B > 0;
+}
+template <int MODE>
+static int launch_rw(const bf16* x, const bf16* w, const float* bias, const bf16* res1, float* colsum, bf16* out,
+                     int B, int H, int W, hipStream_t st) {
+  auto kfn = conv3x3_c64_rw_kernel<MODE>;
+  static bool attr = false;
+  if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, RW_LDS + 256); attr = true; }
+  const int tx = cdiv(W, RW_TW), ty = cdiv(H, RW_TH);
+  const long tiles = (long)B * tx * ty;
+  if (tiles >= (1L << 31)) { s3od_set_error("conv rw: too many tiles"); return 22; }
+  static int ncu = 0;
+  if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
+  const int nwg = (int)std::min<long>(tiles, (long)ncu);       // one persistent workgroup per CU
+  hipLaunchKernelGGL(kfn, dim3(nwg), dim3(256), RW_LDS + 256, st, x, w, bias, res1, colsum, out, H, W, tx, ty, (int)tiles);
+  return s3od_check_launch("conv3x3_c64_rw");
+}
+
 // ---------------------------------------------------------------- halo-tile 3x3 weight gradient
 // dW[co][tap][ci] = sum_px dy[px][co] * x[px + tap][ci] for a 3x3 / stride 1 / pad 1 conv with Cin = 64
 // and Cout = 64 / 96 (the full-resolution decoder convs).  The implicit-GEMM wgrad tiles N = 9*64 into
@@ -642,6 +859,10 @@ int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int C
   ConvGeo g{}; g.B = B; g.SH = H; g.SW = W; g.SC = Cin; g.RH = OH; g.RW = OW; g.KH = KH; g.KW = KW; g.s = stride; g.p = pad;
   const int M = B * OH * OW, N = Cout, K = KH * KW * Cin;
   hipStream_t st = (hipStream_t)stream;
+  if (KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && Cin == 64 && Cout == 64 && !relu_in && !stats &&
+      !scale && !shift && !res1 && !res2 && !pre && !colsum && (act == ACT_NONE || act == ACT_RELU) && rw_ok(dtype, B, H, W))
+    return act == ACT_RELU ? launch_rw<2>((const bf16*)x, (const bf16*)wp, bias, nullptr, nullptr, (bf16*)out, B, H, W, st)
+                           : launch_rw<0>((const bf16*)x, (const bf16*)wp, bias, nullptr, nullptr, (bf16*)out, B, H, W, st);
   if (KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && !relu_in && !stats && Cout == 64 && halo_ok(dtype, Cin, Cout)) {
     RowMap rm = halo_rowmap(H, W);
     const int Mv = B * rm.RH * rm.RW * HT_TH * HT_TW;
@@ -684,6 +905,11 @@ int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
                     const float* bias, const float* scale, const float* shift, int act, const void* res1,
                     const void* res2, void* dx, void* pre, double* stats, float* colsum, const void* wT, void* stream) {
   S3OD_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "conv_dgrad: channels %% 8");
+  if (wT && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && Cin == 64 && Cout == 64 && !bias && !scale &&
+      !shift && !res2 && !pre && !stats && act == ACT_RELU_BWD && res1 && rw_ok(dtype, B, H, W))
+    // stride-1 3x3 data gradient = forward conv of dy with the transposed, tap-reversed weight wT
+    return launch_rw<1>((const bf16*)dy, (const bf16*)wT, nullptr, (const bf16*)res1, colsum, (bf16*)dx, B, H, W,
+                        (hipStream_t)stream);
   if (wT && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && !stats && Cin == 64 && Cout == 64 &&
       halo_ok(dtype, Cout, Cin)) {
     // stride-1 3x3 data gradient = forward conv of dy with the transposed, tap-reversed weight wT
