@@ -333,22 +333,34 @@ static int launch_halo(const bf16* x, const bf16* w, EPI epi, int B, int H, int 
 //     gradient, its rows loaded at the start of the tile), the lane pair (lg, lg^1) trades 4-channel
 //     groups so every lane stores one 16-B run of 8 channels per 16-pixel block; column sums of the
 //     output (bias gradient) go through LDS atomics, one global flush per workgroup.
-constexpr int RW_TH = 8, RW_TW = 32, RW_HC = RW_TW + 2, RW_PX = (RW_TH + 2) * RW_HC;   // 340 halo pixels
-constexpr int RW_PIECES = 44, RW_PPW = RW_PIECES / 4;    // 1 KiB DMA pieces per halo (42.5 KiB + pad), per wave
-constexpr int RW_BUF = RW_PIECES * 1024, RW_LDS = 3 * RW_BUF;     // + 256 B of bias / column sums
-static_assert(RW_PX * 128 <= RW_BUF && RW_LDS + 256 <= 160 * 1024, "register-weight conv LDS budget");
+// Input channels CI = 64 (tile 8 x 32) or 96 (the mask heads' data gradient: tile 8 x 16, 192-B halo rows).
+template <int CI> struct RwShape {
+  static constexpr int TH = 8, TW = CI == 64 ? 32 : 16, HC = TW + 2, PX = (TH + 2) * HC;   // halo pixels
+  static constexpr int ROWB = CI * 2, KK = CI / 32, NPC = TW / 16, PB = 4 * NPC;          // 16-px blocks per wave
+  static constexpr int PIECES = ((PX * ROWB + 4095) / 4096) * 4, PPW = PIECES / 4;        // 1 KiB DMA pieces
+  static constexpr int BUF = PIECES * 1024, LDS = 3 * BUF + 256;                           // + bias / column sums
+  static_assert(LDS <= 160 * 1024, "register-weight conv LDS budget");
+  // 16-B slot of logical chunk c in halo row px (an involution; conflict-free ds_read_b128 for every tap offset,
+  // checked against the gfx950 lane groups): CI 64: c ^ (px & 7); CI 96: XOR of the low 2 bits, groups of 4 kept
+  DEV static int slot(int c, int px) {
+    if constexpr (CI == 64) return c ^ (px & 7);
+    else return (c & ~3) | ((c & 3) ^ ((px ^ (px >> 1)) & 3));
+  }
+};
 
 // MODE 0: out = acc + bias;  MODE 2: out = ReLU(acc + bias);  MODE 1: out = res1 > 0 ? acc : 0, colsum += out
-// Every wave issues a FIXED sequence of vector-memory instructions per tile (11 DMA pieces, 8 mask loads, 8 stores:
+// Every wave issues a FIXED sequence of vector-memory instructions per tile (PPW DMA pieces, PB mask loads, PB stores:
 // dummy pieces / out-of-image lanes use an out-of-range buffer offset instead of a branch), so the counted vmcnt
 // that retires a tile's halo is a per-phase constant.
 typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-template <int MODE>
+template <int MODE, int CI>
 __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                                  const float* __restrict__ bias,
                                                                  const bf16* __restrict__ res1, float* __restrict__ colsum,
                                                                  bf16* __restrict__ out, int H, int W, int tiles_x,
                                                                  int tiles_y, int ntiles) {
+  typedef RwShape<CI> S;
+  constexpr int PB = S::PB, PPW = S::PPW, NPC = S::NPC, HC = S::HC, ROWB = S::ROWB;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int lr = lane & 15, lg = lane >> 4, odd = lg & 1;
@@ -357,55 +369,54 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
   // rows in that XCD's L2); its workgroups stride through it
   const int nwg = gridDim.x, xcd = blockIdx.x & 7, wpx = (nwg + 7 - xcd) >> 3, wi = blockIdx.x >> 3;
   const int t_beg = (int)((long)ntiles * xcd / 8), t_end = (int)((long)ntiles * (xcd + 1) / 8);
-  const long img = (long)H * W * 64;                       // elements per image
+  const long img_i = (long)H * W * CI, img_o = (long)H * W * 64;    // elements per image
 
   // weights -> registers: lane (lr, lg) holds w[co = ch0 + 16 nb + lr][tap][ci = 32 kk + 8 lg .. +7]
-  bf16x8 wr[9][2][2];
+  bf16x8 wr[9][S::KK][2];
 #pragma unroll
   for (int tap = 0; tap < 9; tap++)
 #pragma unroll
-    for (int kk = 0; kk < 2; kk++)
+    for (int kk = 0; kk < S::KK; kk++)
 #pragma unroll
       for (int nb = 0; nb < 2; nb++)
-        wr[tap][kk][nb] = *(const bf16x8*)(w + ((long)(ch0 + nb * 16 + lr) * 9 + tap) * 64 + kk * 32 + lg * 8);
+        wr[tap][kk][nb] = *(const bf16x8*)(w + ((long)(ch0 + nb * 16 + lr) * 9 + tap) * CI + kk * 32 + lg * 8);
 
-  // DMA lane constants: piece p = 11 wave + i covers LDS bytes [1024 p, 1024 p + 1024) of a ring slot, laid out
-  // [px][16-B slot], slot = chunk ^ (px & 7); lane writes bytes 16 lane .. +15 of the piece
-  int dm[RW_PPW];
+  // DMA lane constants: piece p = PPW wave + i covers LDS bytes [1024 p, 1024 p + 1024) of a ring slot, laid out
+  // [px][16-B slot]; lane writes bytes 16 lane .. +15 of the piece = logical chunk slot^-1 of pixel px
+  int dm[PPW];
 #pragma unroll
-  for (int i = 0; i < RW_PPW; i++) {
-    const int b = (wave * RW_PPW + i) * 1024 + lane * 16, px = b >> 7, ch = ((b >> 4) & 7) ^ (px & 7);
-    dm[i] = px < RW_PX ? ((px / RW_HC) << 16) | ((px % RW_HC) << 4) | ch : -1;
+  for (int i = 0; i < PPW; i++) {
+    const int b = (wave * PPW + i) * 1024 + lane * 16, px = b / ROWB, ch = S::slot((b % ROWB) >> 4, px);
+    dm[i] = px < S::PX ? ((px / HC) << 16) | ((px % HC) << 4) | ch : -1;
   }
   auto issue = [&](int tile, int slot) {            // tile >= t_end: dummy pieces (zeros into a free slot)
     const bool live = tile < t_end;
     const int tc = live ? tile : t_beg;
     const int txi = tc % tiles_x, t2 = tc / tiles_x, tyi = t2 % tiles_y, bb = t2 / tiles_y;
-    const int ty0 = tyi * RW_TH - 1, tx0 = txi * RW_TW - 1;
-    const auto r = make_rsrc(x + bb * img, (unsigned long)img * 2);
-    char* dst = smem + slot * RW_BUF + wave * RW_PPW * 1024;
+    const int ty0 = tyi * S::TH - 1, tx0 = txi * S::TW - 1;
+    const auto r = make_rsrc(x + bb * img_i, (unsigned long)img_i * 2);
+    char* dst = smem + slot * S::BUF + wave * PPW * 1024;
 #pragma unroll
-    for (int i = 0; i < RW_PPW; i++) {
+    for (int i = 0; i < PPW; i++) {
       const int v = dm[i], gy = ty0 + (v >> 16), gx = tx0 + ((v >> 4) & 0xfff);
       const bool ok = live && v >= 0 && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
-      blds16(r, ok ? (unsigned)((gy * W + gx) * 128 + (v & 15) * 16) : 0x80000000u, dst + i * 1024);
+      blds16(r, ok ? (unsigned)((gy * W + gx) * ROWB + (v & 15) * 16) : 0x80000000u, dst + i * 1024);
     }
   };
-  // halo fragment addresses: px = L + off (L = row0 * 34 + lr per lane, off compile-time per (pb, tap)), byte
-  // px * 128 + (((4 kk + lg) ^ (px & 7)) << 4) = yb[(off & 7)][kk] + 128 off  (the XOR term depends on the lane
-  // and on off & 7 only), so every ds_read is a per-lane base + an immediate
-  int yb[8][2];
+  // halo fragment addresses: px = L + off (L = row0 * HC + lr per lane, off compile-time per (block, tap)); the
+  // slot term depends on the lane and on off & 7 only, so yb[off & 7][kk] + ROWB * off = per-lane base + immediate
+  int yb[8][S::KK];
   {
-    const int L = row0 * RW_HC + lr;
+    const int L = row0 * HC + lr;
 #pragma unroll
     for (int j = 0; j < 8; j++)
 #pragma unroll
-      for (int kk = 0; kk < 2; kk++) yb[j][kk] = L * 128 + (((kk * 4 + lg) ^ ((L + j) & 7)) << 4);
+      for (int kk = 0; kk < S::KK; kk++) yb[j][kk] = L * ROWB + 16 * S::slot(kk * 4 + lg, L + j);
   }
   // after the lane-pair trade in the epilogue a lane owns channels cb .. cb+7 of its pixel
   const int cb = ch0 + (odd ? 16 : 0) + 8 * (lg >> 1);
-  // 64 floats after the ring: the bias (MODE 0, the accumulators' initial value) or the column sums (MODE 1)
-  float* aux = (float*)(smem + RW_LDS);
+  // 64 floats after the ring: the bias (MODE 0/2, the accumulators' initial value) or the column sums (MODE 1)
+  float* aux = (float*)(smem + 3 * S::BUF);
   if (tid < 64) aux[tid] = (MODE != 1 && bias) ? bias[tid] : 0.f;
   __syncthreads();
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -415,72 +426,71 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
   issue(tile + wpx, 1);
   for (; tile < t_end; tile += wpx, k++) {
     const int txi = tile % tiles_x, t2 = tile / tiles_x, tyi = t2 % tiles_y, bb = t2 / tiles_y;
-    const auto ro = make_rsrc(out + bb * img, (unsigned long)img * 2);
-    unsigned po[8];                                   // byte offset of this lane's 8-channel run per 16-px block (or OOB)
+    const auto ro = make_rsrc(out + bb * img_o, (unsigned long)img_o * 2);
+    unsigned po[PB];                                  // byte offset of this lane's 8-channel run per 16-px block (or OOB)
 #pragma unroll
-    for (int pb = 0; pb < 8; pb++) {
-      const int gy = tyi * RW_TH + row0 + (pb >> 1), gx = txi * RW_TW + (pb & 1) * 16 + lr;
+    for (int pb = 0; pb < PB; pb++) {
+      const int gy = tyi * S::TH + row0 + pb / NPC, gx = txi * S::TW + (pb % NPC) * 16 + lr;
       po[pb] = (gy < H && gx < W) ? (unsigned)((gy * W + gx) * 128 + cb * 2) : 0x80000000u;
     }
     // data-gradient mask runs of this tile, issued before the next halo's DMA (their wait leaves it in flight)
-    u32x4v rm_[8];
+    u32x4v rm_[PB];
     if constexpr (MODE == 1) {
-      const auto rr = make_rsrc(res1 + bb * img, (unsigned long)img * 2);
+      const auto rr = make_rsrc(res1 + bb * img_o, (unsigned long)img_o * 2);
 #pragma unroll
-      for (int pb = 0; pb < 8; pb++) rm_[pb] = __builtin_amdgcn_raw_buffer_load_b128(rr, po[pb], 0, 0);
+      for (int pb = 0; pb < PB; pb++) rm_[pb] = __builtin_amdgcn_raw_buffer_load_b128(rr, po[pb], 0, 0);
     }
     // retire this tile's halo (own pieces): the vector-memory ops issued after them are a per-phase constant
-    //   k = 0: next halo (11) [+ masks 8];  k = 1: [masks 8,] halo 11, stores 8 [, masks 8];
-    //   k >= 2: stores 8 [, masks 8], halo 11, stores 8 [, masks 8]
-    if (k == 0) { if constexpr (MODE == 1) wait_vmcnt<RW_PPW + 8>(); else wait_vmcnt<RW_PPW>(); }
-    else if (k == 1) { if constexpr (MODE == 1) wait_vmcnt<8 + RW_PPW + 8 + 8>(); else wait_vmcnt<RW_PPW + 8>(); }
-    else { if constexpr (MODE == 1) wait_vmcnt<8 + 8 + RW_PPW + 8 + 8>(); else wait_vmcnt<8 + RW_PPW + 8>(); }
+    //   k = 0: next halo [+ masks];  k = 1: [masks,] halo, stores [, masks];  k >= 2: stores [, masks], halo, stores [, masks]
+    if (k == 0) { if constexpr (MODE == 1) wait_vmcnt<PPW + PB>(); else wait_vmcnt<PPW>(); }
+    else if (k == 1) { if constexpr (MODE == 1) wait_vmcnt<PB + PPW + PB + PB>(); else wait_vmcnt<PPW + PB>(); }
+    else { if constexpr (MODE == 1) wait_vmcnt<PB + PB + PPW + PB + PB>(); else wait_vmcnt<PB + PPW + PB>(); }
     __builtin_amdgcn_s_barrier();                     // every wave's pieces landed; every wave done with slot k-1
     asm volatile("" ::: "memory");
     issue(tile + 2 * wpx, (k + 2) % 3);
-    const char* hb = smem + (k % 3) * RW_BUF;
-    f32x4 acc[8][2];                                  // acc[pb][nb]: D[co = ch0 + 16 nb + 4 lg + e][px = 16 pb + lr]
+    const char* hb = smem + (k % 3) * S::BUF;
+    f32x4 acc[PB][2];                                 // acc[pb][nb]: D[co = ch0 + 16 nb + 4 lg + e][px = block pb, lr]
 #pragma unroll
     for (int nb = 0; nb < 2; nb++) {
       const f32x4 b0 = MODE != 1 ? *(const f32x4*)(aux + ch0 + nb * 16 + 4 * lg) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int pb = 0; pb < 8; pb++) acc[pb][nb] = b0;
+      for (int pb = 0; pb < PB; pb++) acc[pb][nb] = b0;
     }
-    // 18 (tap, k-half) steps of 16 MFMAs; the next step's 8 halo fragments are read before this step's MFMAs
-    auto rd = [&](int st, bf16x8 (&fa)[8]) {
-      const int tap = st >> 1, kk = st & 1, dy = tap / 3, dx = tap - 3 * (tap / 3);
+    // 9 * KK (tap, k-chunk) steps of 2 PB MFMAs; the next step's PB halo fragments are read before this step's MFMAs
+    constexpr int NST = 9 * S::KK;
+    auto rd = [&](int st, bf16x8 (&fa)[PB]) {
+      const int tap = st / S::KK, kk = st % S::KK, dy = tap / 3, dx = tap - 3 * (tap / 3);
 #pragma unroll
-      for (int pb = 0; pb < 8; pb++) {
-        const int off = ((pb >> 1) + dy) * RW_HC + (pb & 1) * 16 + dx;
-        fa[pb] = *(const bf16x8*)(hb + yb[off & 7][kk] + off * 128);
+      for (int pb = 0; pb < PB; pb++) {
+        const int off = (pb / NPC + dy) * HC + (pb % NPC) * 16 + dx;
+        fa[pb] = *(const bf16x8*)(hb + yb[off & 7][kk] + off * ROWB);
       }
     };
-    auto mm = [&](int st, const bf16x8 (&fa)[8]) {
+    auto mm = [&](int st, const bf16x8 (&fa)[PB]) {
 #pragma unroll
-      for (int pb = 0; pb < 8; pb++)
+      for (int pb = 0; pb < PB; pb++)
 #pragma unroll
         for (int nb = 0; nb < 2; nb++)
-          acc[pb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[st >> 1][st & 1][nb], fa[pb], acc[pb][nb], 0, 0, 0);
+          acc[pb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[st / S::KK][st % S::KK][nb], fa[pb], acc[pb][nb], 0, 0, 0);
     };
-    bf16x8 fa0[8], fa1[8];
+    bf16x8 fa0[PB], fa1[PB];
     rd(0, fa0);
 #pragma unroll
-    for (int st = 0; st < 18; st += 2) {
-      rd(st + 1, fa1);
+    for (int st = 0; st < NST; st += 2) {
+      if (st + 1 < NST) rd(st + 1, fa1);
       __builtin_amdgcn_sched_barrier(0);
       mm(st, fa0);
       __builtin_amdgcn_sched_barrier(0);
-      if (st + 2 < 18) rd(st + 2, fa0);
+      if (st + 2 < NST) rd(st + 2, fa0);
       __builtin_amdgcn_sched_barrier(0);
-      mm(st + 1, fa1);
+      if (st + 1 < NST) mm(st + 1, fa1);
       __builtin_amdgcn_sched_barrier(0);
     }
-    // epilogue: lane holds out[px = 16 pb + lr][co = ch0 + 16 nb + 4 lg .. +3]; the pair (lg, lg^1) trades
-    // so the even lane keeps nb 0 (channels cb .. cb+7) and the odd lane nb 1
+    // epilogue: lane holds out[px = block pb, lr][co = ch0 + 16 nb + 4 lg .. +3]; v_permlane16_swap trades rows 1 / 3
+    // of the first operand with rows 0 / 2 of the second (row = 16 lanes = one lg): the even lg keeps its nb 0 and
+    // receives the odd partner's nb 0, the odd lg keeps nb 1 and receives the even's -> 8 channels cb .. cb+7
 #pragma unroll
-    for (int pb = 0; pb < 8; pb++) {
-      // v_permlane16_swap: rows 1 / 3 of the first operand <-> rows 0 / 2 of the second (row = 16 lanes = one lg):
-      // even lg keeps its nb 0 and receives the odd partner's nb 0, the odd lg keeps nb 1 and receives the even's
+    for (int pb = 0; pb < PB; pb++) {
       float o[8];
 #pragma unroll
       for (int e = 0; e < 4; e++) {
@@ -519,21 +529,22 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
 // S3OD_CONV_RW=0 disables the path (read per call: an A/B inside one process)
 static bool rw_ok(int dtype, int B, int H, int W) {
   const char* e = getenv("S3OD_CONV_RW");
-  return dtype == S3OD_BF16 && !(e && atoi(e) == 0) && (long)H * W * 128 < (1L << 31) && B > 0;
+  return dtype == S3OD_BF16 && !(e && atoi(e) == 0) && (long)H * W * 192 < (1L << 31) && B > 0;
 }
-template <int MODE>
+template <int MODE, int CI>
 static int launch_rw(const bf16* x, const bf16* w, const float* bias, const bf16* res1, float* colsum, bf16* out,
                      int B, int H, int W, hipStream_t st) {
-  auto kfn = conv3x3_c64_rw_kernel<MODE>;
+  typedef RwShape<CI> S;
+  auto kfn = conv3x3_c64_rw_kernel<MODE, CI>;
   static bool attr = false;
-  if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, RW_LDS + 256); attr = true; }
-  const int tx = cdiv(W, RW_TW), ty = cdiv(H, RW_TH);
+  if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS); attr = true; }
+  const int tx = cdiv(W, S::TW), ty = cdiv(H, S::TH);
   const long tiles = (long)B * tx * ty;
   if (tiles >= (1L << 31)) { s3od_set_error("conv rw: too many tiles"); return 22; }
   static int ncu = 0;
   if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
   const int nwg = (int)std::min<long>(tiles, (long)ncu);       // one persistent workgroup per CU
-  hipLaunchKernelGGL(kfn, dim3(nwg), dim3(256), RW_LDS + 256, st, x, w, bias, res1, colsum, out, H, W, tx, ty, (int)tiles);
+  hipLaunchKernelGGL(kfn, dim3(nwg), dim3(256), S::LDS, st, x, w, bias, res1, colsum, out, H, W, tx, ty, (int)tiles);
   return s3od_check_launch("conv3x3_c64_rw");
 }
 
@@ -861,8 +872,8 @@ int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int C
   hipStream_t st = (hipStream_t)stream;
   if (KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && Cin == 64 && Cout == 64 && !relu_in && !stats &&
       !scale && !shift && !res1 && !res2 && !pre && !colsum && (act == ACT_NONE || act == ACT_RELU) && rw_ok(dtype, B, H, W))
-    return act == ACT_RELU ? launch_rw<2>((const bf16*)x, (const bf16*)wp, bias, nullptr, nullptr, (bf16*)out, B, H, W, st)
-                           : launch_rw<0>((const bf16*)x, (const bf16*)wp, bias, nullptr, nullptr, (bf16*)out, B, H, W, st);
+    return act == ACT_RELU ? launch_rw<2, 64>((const bf16*)x, (const bf16*)wp, bias, nullptr, nullptr, (bf16*)out, B, H, W, st)
+                           : launch_rw<0, 64>((const bf16*)x, (const bf16*)wp, bias, nullptr, nullptr, (bf16*)out, B, H, W, st);
   if (KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && !relu_in && !stats && Cout == 64 && halo_ok(dtype, Cin, Cout)) {
     RowMap rm = halo_rowmap(H, W);
     const int Mv = B * rm.RH * rm.RW * HT_TH * HT_TW;
@@ -905,11 +916,13 @@ int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
                     const float* bias, const float* scale, const float* shift, int act, const void* res1,
                     const void* res2, void* dx, void* pre, double* stats, float* colsum, const void* wT, void* stream) {
   S3OD_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "conv_dgrad: channels %% 8");
-  if (wT && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && Cin == 64 && Cout == 64 && !bias && !scale &&
-      !shift && !res2 && !pre && !stats && act == ACT_RELU_BWD && res1 && rw_ok(dtype, B, H, W))
-    // stride-1 3x3 data gradient = forward conv of dy with the transposed, tap-reversed weight wT
-    return launch_rw<1>((const bf16*)dy, (const bf16*)wT, nullptr, (const bf16*)res1, colsum, (bf16*)dx, B, H, W,
-                        (hipStream_t)stream);
+  if (wT && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && Cin == 64 && (Cout == 64 || Cout == 96) &&
+      !bias && !scale && !shift && !res2 && !pre && !stats && act == ACT_RELU_BWD && res1 && rw_ok(dtype, B, H, W))
+    // stride-1 3x3 data gradient = forward conv of dy with the transposed, tap-reversed weight wT ([Cin][3][3][Cout])
+    return Cout == 64 ? launch_rw<1, 64>((const bf16*)dy, (const bf16*)wT, nullptr, (const bf16*)res1, colsum, (bf16*)dx, B, H,
+                                         W, (hipStream_t)stream)
+                      : launch_rw<1, 96>((const bf16*)dy, (const bf16*)wT, nullptr, (const bf16*)res1, colsum, (bf16*)dx, B, H,
+                                         W, (hipStream_t)stream);
   if (wT && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && !stats && Cin == 64 && Cout == 64 &&
       halo_ok(dtype, Cout, Cin)) {
     // stride-1 3x3 data gradient = forward conv of dy with the transposed, tap-reversed weight wT

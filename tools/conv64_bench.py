@@ -38,6 +38,9 @@ def main():
     wT = w.flip(1, 2).permute(3, 1, 2, 0).contiguous()                                 # [Cin][3][3][Cout]
     bias = torch.randn(64, device="cuda", generator=g) * 0.1
     res1 = torch.randn(B, H, W, 64, device="cuda", generator=g).bfloat16()
+    dy96 = torch.randn(B, H, W, 96, device="cuda", generator=g).bfloat16()
+    w96 = (torch.randn(96, 3, 3, 64, device="cuda", generator=g) * 0.06).bfloat16()    # heads conv [96][3][3][64]
+    w96T = w96.flip(1, 2).permute(3, 1, 2, 0).contiguous()                             # [64][3][3][96]
     outs = {}
     fl = 2.0 * B * H * W * 64 * 64 * 9
 
@@ -49,6 +52,10 @@ def main():
         lib()("s3od_conv_dgrad", BF16, B, H, W, 64, H, W, 64, 3, 3, 1, 1, x, w, None, None, None, ACT_RELU_BWD, res1,
               None, o, None, None, cs, wT, stream())
 
+    def dgrad96(o, cs):
+        lib()("s3od_conv_dgrad", BF16, B, H, W, 64, H, W, 96, 3, 3, 1, 1, dy96, w96, None, None, None, ACT_RELU_BWD, res1,
+              None, o, None, None, cs, w96T, stream())
+
     for rnd in range(3):
         for rw in ("0", "1"):
             os.environ["S3OD_CONV_RW"] = rw
@@ -57,15 +64,20 @@ def main():
             cs = torch.zeros(64, device="cuda")
             tf = timeit(lambda: fwd(of))
             td = timeit(lambda: dgrad(od, cs))
+            o96 = torch.empty_like(of)
+            t96 = timeit(lambda: dgrad96(o96, cs))
             cs.zero_()
             dgrad(od, cs)
+            cs96 = torch.zeros(64, device="cuda")
+            dgrad96(o96, cs96)
             torch.cuda.synchronize()
-            outs[rw] = (of, od, cs.clone())
+            outs[rw] = (of, od, cs.clone(), o96, cs96)
             by_f = B * H * W * 64 * 2 * 2
             by_d = B * H * W * 64 * 2 * 3
             print(f"round {rnd} RW={rw}: fwd {tf * 1e6:8.1f} us ({fl / tf / 1e12:6.1f} TF/s, {by_f / tf / 1e9:6.0f} GB/s) | "
-                  f"dgrad {td * 1e6:8.1f} us ({fl / td / 1e12:6.1f} TF/s, {by_d / td / 1e9:6.0f} GB/s)", flush=True)
-    for i, name in enumerate(("fwd", "dgrad", "colsum")):
+                  f"dgrad {td * 1e6:8.1f} us ({fl / td / 1e12:6.1f} TF/s, {by_d / td / 1e9:6.0f} GB/s) | dgrad 64<-96 {t96 * 1e6:8.1f} us "
+                  f"({fl * 1.5 / t96 / 1e12:6.1f} TF/s, {by_d * 3.5 / 3 / t96 / 1e9:6.0f} GB/s)", flush=True)
+    for i, name in enumerate(("fwd", "dgrad", "colsum", "dgrad 64<-96", "colsum 64<-96")):
         a, b = outs["0"][i].float(), outs["1"][i].float()
         print(f"{name}: max |rw - igemm| / max|igemm| = {float((a - b).abs().max() / b.abs().max().clamp_min(1e-9)):.3e}")
 
