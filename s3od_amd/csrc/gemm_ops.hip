@@ -338,7 +338,7 @@ template <int CI> struct RwShape {
   static constexpr int TH = 8, TW = CI == 64 ? 32 : 16, HC = TW + 2, PX = (TH + 2) * HC;   // halo pixels
   static constexpr int ROWB = CI * 2, KK = CI / 32, NPC = TW / 16, PB = 4 * NPC;          // 16-px blocks per wave
   static constexpr int PIECES = ((PX * ROWB + 4095) / 4096) * 4, PPW = PIECES / 4;        // 1 KiB DMA pieces
-  static constexpr int BUF = PIECES * 1024, LDS = 3 * BUF + 256;                           // + bias / column sums
+  static constexpr int BUF = PIECES * 1024, LDS = 3 * BUF + 2048;       // + bias / column sums / head partials
   static_assert(LDS <= 160 * 1024, "register-weight conv LDS budget");
   // 16-B slot of logical chunk c in halo row px (an involution; conflict-free ds_read_b128 for every tap offset,
   // checked against the gfx950 lane groups): CI 64: c ^ (px & 7); CI 96: XOR of the low 2 bits, groups of 4 kept
@@ -348,37 +348,44 @@ template <int CI> struct RwShape {
   }
 };
 
-// MODE 0: out = acc + bias;  MODE 2: out = ReLU(acc + bias);  MODE 1: out = res1 > 0 ? acc : 0, colsum += out
+// MODE 0: out = acc + bias;  MODE 2: out = ReLU(acc + bias);  MODE 1: out = res1 > 0 ? acc : 0, colsum += out;
+// MODE 3: the 3 mask heads (src/s3od/model.py:440-452,461-467): 96 output channels (48 per wave, NB = 3),
+//   h = ReLU(acc + b1) -> hsave (bf16 [px][96]) and logit_k = b2[k] + h[32k .. 32k+31] . w2[k] -> logits [B][3][H][W];
+//   head 1 straddles the two waves of a row group: the odd wave's part goes through LDS (one extra barrier)
 // Every wave issues a FIXED sequence of vector-memory instructions per tile (PPW DMA pieces, PB mask loads, PB stores:
 // dummy pieces / out-of-image lanes use an out-of-range buffer offset instead of a branch), so the counted vmcnt
 // that retires a tile's halo is a per-phase constant.
 typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
 template <int MODE, int CI>
 __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                                  const float* __restrict__ bias,
                                                                  const bf16* __restrict__ res1, float* __restrict__ colsum,
                                                                  bf16* __restrict__ out, int H, int W, int tiles_x,
-                                                                 int tiles_y, int ntiles) {
+                                                                 int tiles_y, int ntiles, const float* __restrict__ w2,
+                                                                 const float* __restrict__ b2, float* __restrict__ logits) {
   typedef RwShape<CI> S;
   constexpr int PB = S::PB, PPW = S::PPW, NPC = S::NPC, HC = S::HC, ROWB = S::ROWB;
+  constexpr int NB = MODE == 3 ? 3 : 2, CO = 32 * NB;     // 16-channel blocks per wave / output channels
+  static_assert(MODE != 3 || (CI == 64 && NPC == 2), "mask heads: 64 input channels, 8 x 32 tiles");
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int lr = lane & 15, lg = lane >> 4, odd = lg & 1;
-  const int row0 = 4 * (wave >> 1), ch0 = 32 * (wave & 1);      // this wave's output rows / channels
+  const int row0 = 4 * (wave >> 1), ch0 = 16 * NB * (wave & 1);   // this wave's output rows / channels
   // tiles: XCD x = blockIdx % 8 owns the contiguous range [x*n/8, (x+1)*n/8) (neighbouring tiles share halo
   // rows in that XCD's L2); its workgroups stride through it
   const int nwg = gridDim.x, xcd = blockIdx.x & 7, wpx = (nwg + 7 - xcd) >> 3, wi = blockIdx.x >> 3;
   const int t_beg = (int)((long)ntiles * xcd / 8), t_end = (int)((long)ntiles * (xcd + 1) / 8);
-  const long img_i = (long)H * W * CI, img_o = (long)H * W * 64;    // elements per image
+  const long img_i = (long)H * W * CI, img_o = (long)H * W * CO;    // elements per image
 
   // weights -> registers: lane (lr, lg) holds w[co = ch0 + 16 nb + lr][tap][ci = 32 kk + 8 lg .. +7]
-  bf16x8 wr[9][S::KK][2];
+  bf16x8 wr[9][S::KK][NB];
 #pragma unroll
   for (int tap = 0; tap < 9; tap++)
 #pragma unroll
     for (int kk = 0; kk < S::KK; kk++)
 #pragma unroll
-      for (int nb = 0; nb < 2; nb++)
+      for (int nb = 0; nb < NB; nb++)
         wr[tap][kk][nb] = *(const bf16x8*)(w + ((long)(ch0 + nb * 16 + lr) * 9 + tap) * CI + kk * 32 + lg * 8);
 
   // DMA lane constants: piece p = PPW wave + i covers LDS bytes [1024 p, 1024 p + 1024) of a ring slot, laid out
@@ -416,8 +423,13 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
   // after the lane-pair trade in the epilogue a lane owns channels cb .. cb+7 of its pixel
   const int cb = ch0 + (odd ? 16 : 0) + 8 * (lg >> 1);
   // 64 floats after the ring: the bias (MODE 0/2, the accumulators' initial value) or the column sums (MODE 1)
+  // MODE 3: aux[0..95] = b1, aux[96..191] = w2, aux[192..194] = b2, aux[256..511] = head-1 partials [8 rows][32 px]
   float* aux = (float*)(smem + 3 * S::BUF);
-  if (tid < 64) aux[tid] = (MODE != 1 && bias) ? bias[tid] : 0.f;
+  if (tid < CO) aux[tid] = (MODE != 1 && bias) ? bias[tid] : 0.f;
+  if constexpr (MODE == 3) {
+    if (tid < 96) aux[96 + tid] = w2[tid];
+    if (tid < 3) aux[192 + tid] = b2[tid];
+  }
   __syncthreads();
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
@@ -426,12 +438,12 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
   issue(tile + wpx, 1);
   for (; tile < t_end; tile += wpx, k++) {
     const int txi = tile % tiles_x, t2 = tile / tiles_x, tyi = t2 % tiles_y, bb = t2 / tiles_y;
-    const auto ro = make_rsrc(out + bb * img_o, (unsigned long)img_o * 2);
+    const auto ro = make_rsrc(out + bb * img_o, out ? (unsigned long)img_o * 2 : 0ul);   // MODE 3: hsave is optional
     unsigned po[PB];                                  // byte offset of this lane's 8-channel run per 16-px block (or OOB)
 #pragma unroll
     for (int pb = 0; pb < PB; pb++) {
       const int gy = tyi * S::TH + row0 + pb / NPC, gx = txi * S::TW + (pb % NPC) * 16 + lr;
-      po[pb] = (gy < H && gx < W) ? (unsigned)((gy * W + gx) * 128 + cb * 2) : 0x80000000u;
+      po[pb] = (gy < H && gx < W) ? (unsigned)((gy * W + gx) * (CO * 2) + cb * 2) : 0x80000000u;
     }
     // data-gradient mask runs of this tile, issued before the next halo's DMA (their wait leaves it in flight)
     u32x4v rm_[PB];
@@ -442,16 +454,18 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
     }
     // retire this tile's halo (own pieces): the vector-memory ops issued after them are a per-phase constant
     //   k = 0: next halo [+ masks];  k = 1: [masks,] halo, stores [, masks];  k >= 2: stores [, masks], halo, stores [, masks]
+    //   (MODE 3 stores 2 PB hsave runs + 8 logit rows = 3 PB per tile)
+    constexpr int NS = MODE == 3 ? 3 * PB : PB;       // stores per tile
     if (k == 0) { if constexpr (MODE == 1) wait_vmcnt<PPW + PB>(); else wait_vmcnt<PPW>(); }
-    else if (k == 1) { if constexpr (MODE == 1) wait_vmcnt<PB + PPW + PB + PB>(); else wait_vmcnt<PPW + PB>(); }
-    else { if constexpr (MODE == 1) wait_vmcnt<PB + PB + PPW + PB + PB>(); else wait_vmcnt<PB + PPW + PB>(); }
+    else if (k == 1) { if constexpr (MODE == 1) wait_vmcnt<PB + PPW + PB + PB>(); else wait_vmcnt<PPW + NS>(); }
+    else { if constexpr (MODE == 1) wait_vmcnt<PB + PB + PPW + PB + PB>(); else wait_vmcnt<NS + PPW + NS>(); }
     __builtin_amdgcn_s_barrier();                     // every wave's pieces landed; every wave done with slot k-1
     asm volatile("" ::: "memory");
     issue(tile + 2 * wpx, (k + 2) % 3);
     const char* hb = smem + (k % 3) * S::BUF;
-    f32x4 acc[PB][2];                                 // acc[pb][nb]: D[co = ch0 + 16 nb + 4 lg + e][px = block pb, lr]
+    f32x4 acc[PB][NB];                                // acc[pb][nb]: D[co = ch0 + 16 nb + 4 lg + e][px = block pb, lr]
 #pragma unroll
-    for (int nb = 0; nb < 2; nb++) {
+    for (int nb = 0; nb < NB; nb++) {
       const f32x4 b0 = MODE != 1 ? *(const f32x4*)(aux + ch0 + nb * 16 + 4 * lg) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int pb = 0; pb < PB; pb++) acc[pb][nb] = b0;
@@ -470,7 +484,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
 #pragma unroll
       for (int pb = 0; pb < PB; pb++)
 #pragma unroll
-        for (int nb = 0; nb < 2; nb++)
+        for (int nb = 0; nb < NB; nb++)
           acc[pb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[st / S::KK][st % S::KK][nb], fa[pb], acc[pb][nb], 0, 0, 0);
     };
     bf16x8 fa0[PB], fa1[PB];
@@ -486,6 +500,71 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
       if (st + 1 < NST) mm(st + 1, fa1);
       __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (MODE == 3) {
+      // h = ReLU(acc) (b1 was the initial value); hsave: channels cb .. cb+7 (nb 0 / 1 traded as below) and
+      // ch0 + 32 + 4 lg .. +3 (nb 2); head partials: per 16-channel block, summed over the 4 lg lanes
+      float hp[PB][3];
+#pragma unroll
+      for (int pb = 0; pb < PB; pb++) {
+        float v[3][4];
+#pragma unroll
+        for (int nb = 0; nb < 3; nb++)
+#pragma unroll
+          for (int e = 0; e < 4; e++) v[nb][e] = fmaxf(acc[pb][nb][e], 0.f);
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[0][e]), __float_as_uint(v[1][e]), false, false);
+          o[e] = __uint_as_float(sw[0]);
+          o[4 + e] = __uint_as_float(sw[1]);
+        }
+        bf16x8 ob;
+#pragma unroll
+        for (int e = 0; e < 8; e++) ob[e] = (bf16)o[e];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, ob), ro, po[pb], 0, 0);
+        const unsigned p2 = po[pb] == 0x80000000u ? po[pb] : po[pb] - cb * 2 + (ch0 + 32 + 4 * lg) * 2;
+        const bf16x4 o2 = {(bf16)v[2][0], (bf16)v[2][1], (bf16)v[2][2], (bf16)v[2][3]};
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, o2), ro, p2, 0, 0);
+#pragma unroll
+        for (int nb = 0; nb < 3; nb++) {
+          float d = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; e++) d += v[nb][e] * aux[96 + ch0 + 16 * nb + 4 * lg + e];
+          d += __shfl_xor(d, 16);
+          d += __shfl_xor(d, 32);
+          hp[pb][nb] = d;
+        }
+      }
+      // wave half 0 (channels 0-47): head 0 = blocks 0 + 1, head 1 = block 2 + the odd wave's block 0;
+      // half 1 (48-95): head 2 = blocks 1 + 2
+      float* part = aux + 256 + (row0 + 0) * 32;
+      if (wave & 1) {
+#pragma unroll
+        for (int pb = 0; pb < PB; pb++)
+          if (lg == 0) part[(pb / NPC) * 32 + (pb % NPC) * 16 + lr] = hp[pb][0];
+      }
+      lds_barrier();
+      const auto rl = make_rsrc(logits + (long)bb * 3 * H * W, (unsigned long)3 * H * W * 4);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        // lanes lg 0 / 1 store the row's two 16-pixel blocks (64 + 64 contiguous bytes); lg 2 / 3 are out of range
+        const int gy = tyi * S::TH + row0 + r, gx = txi * S::TW + (lg & 1) * 16 + lr;
+        const bool ok = lg < 2 && gy < H && gx < W;
+        const int pb = 2 * r + (lg & 1);
+        const unsigned base = (unsigned)(gy * W + gx) * 4;
+        if (!(wave & 1)) {
+          const float l0 = aux[192] + hp[2 * r][0] + hp[2 * r][1], l0b = aux[192] + hp[2 * r + 1][0] + hp[2 * r + 1][1];
+          const float l1 = aux[193] + hp[2 * r][2] + part[r * 32 + lr], l1b = aux[193] + hp[2 * r + 1][2] + part[r * 32 + 16 + lr];
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((lg & 1) ? l0b : l0), rl, ok ? base : 0x80000000u, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((lg & 1) ? l1b : l1), rl, ok ? base + (unsigned)H * W * 4 : 0x80000000u, 0, 0);
+        } else {
+          const float l2 = aux[194] + hp[2 * r][1] + hp[2 * r][2], l2b = aux[194] + hp[2 * r + 1][1] + hp[2 * r + 1][2];
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((lg & 1) ? l2b : l2), rl, ok ? base + 2u * H * W * 4 : 0x80000000u, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(0u, rl, 0x80000000u, 0, 0);   // keeps the per-tile store count uniform
+        }
+        (void)pb;
+      }
+    } else {
     // epilogue: lane holds out[px = block pb, lr][co = ch0 + 16 nb + 4 lg .. +3]; v_permlane16_swap trades rows 1 / 3
     // of the first operand with rows 0 / 2 of the second (row = 16 lanes = one lg): the even lg keeps its nb 0 and
     // receives the odd partner's nb 0, the odd lg keeps nb 1 and receives the even's -> 8 channels cb .. cb+7
@@ -512,6 +591,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
       for (int e = 0; e < 8; e++) ob[e] = (bf16)o[e];
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, ob), ro, po[pb], 0, 0);
     }
+    }
   }
   if (MODE == 1 && colsum) {                          // 16 lanes (lr) -> 1, LDS atomics, one global add per channel
 #pragma unroll
@@ -533,7 +613,8 @@ static bool rw_ok(int dtype, int B, int H, int W) {
 }
 template <int MODE, int CI>
 static int launch_rw(const bf16* x, const bf16* w, const float* bias, const bf16* res1, float* colsum, bf16* out,
-                     int B, int H, int W, hipStream_t st) {
+                     int B, int H, int W, hipStream_t st, const float* w2 = nullptr, const float* b2 = nullptr,
+                     float* logits = nullptr) {
   typedef RwShape<CI> S;
   auto kfn = conv3x3_c64_rw_kernel<MODE, CI>;
   static bool attr = false;
@@ -544,7 +625,8 @@ static int launch_rw(const bf16* x, const bf16* w, const float* bias, const bf16
   static int ncu = 0;
   if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
   const int nwg = (int)std::min<long>(tiles, (long)ncu);       // one persistent workgroup per CU
-  hipLaunchKernelGGL(kfn, dim3(nwg), dim3(256), S::LDS, st, x, w, bias, res1, colsum, out, H, W, tx, ty, (int)tiles);
+  hipLaunchKernelGGL(kfn, dim3(nwg), dim3(256), S::LDS, st, x, w, bias, res1, colsum, out, H, W, tx, ty, (int)tiles, w2, b2,
+                     logits);
   return s3od_check_launch("conv3x3_c64_rw");
 }
 
@@ -1024,6 +1106,8 @@ int s3od_mask_heads_fwd(int dtype, int B, int H, int W, int NM, const void* feat
   ConvGeo g{}; g.B = B; g.SH = H; g.SW = W; g.SC = 64; g.RH = H; g.RW = W; g.KH = 3; g.KW = 3; g.s = 1; g.p = 1;
   const int M = B * H * W, N = 32 * NM, K = 9 * 64;
   hipStream_t st = (hipStream_t)stream;
+  if (N == 96 && rw_ok(dtype, B, H, W) && (long)3 * H * W * 4 < (1L << 31))
+    return launch_rw<3, 64>((const bf16*)feat, (const bf16*)w1p, b1, nullptr, nullptr, (bf16*)hsave, B, H, W, st, w2, b2, logits);
   if (N == 96 && halo_ok(dtype, 64, N)) {
     RowMap rm = halo_rowmap(H, W);
     EpiHeads<bf16> e{logits, (bf16*)hsave, b1, w2, b2, B * rm.RH * rm.RW * HT_TH * HT_TW, H * W, NM, rm};

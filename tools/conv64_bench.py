@@ -41,6 +41,10 @@ def main():
     dy96 = torch.randn(B, H, W, 96, device="cuda", generator=g).bfloat16()
     w96 = (torch.randn(96, 3, 3, 64, device="cuda", generator=g) * 0.06).bfloat16()    # heads conv [96][3][3][64]
     w96T = w96.flip(1, 2).permute(3, 1, 2, 0).contiguous()                             # [64][3][3][96]
+    hw1 = (torch.randn(96, 3, 3, 64, device="cuda", generator=g) * 0.06).bfloat16()
+    hb1 = torch.randn(96, device="cuda", generator=g) * 0.1
+    hw2 = torch.randn(3, 32, device="cuda", generator=g) * 0.2
+    hb2 = torch.randn(3, device="cuda", generator=g) * 0.1
     outs = {}
     fl = 2.0 * B * H * W * 64 * 64 * 9
 
@@ -55,6 +59,9 @@ def main():
     def dgrad96(o, cs):
         lib()("s3od_conv_dgrad", BF16, B, H, W, 64, H, W, 96, 3, 3, 1, 1, dy96, w96, None, None, None, ACT_RELU_BWD, res1,
               None, o, None, None, cs, w96T, stream())
+
+    def heads(lg, hs):
+        lib()("s3od_mask_heads_fwd", BF16, B, H, W, 3, x, hw1, hb1, hw2, hb2, lg, hs, stream())
 
     for rnd in range(3):
         for rw in ("0", "1"):
@@ -71,13 +78,17 @@ def main():
             cs96 = torch.zeros(64, device="cuda")
             dgrad96(o96, cs96)
             torch.cuda.synchronize()
-            outs[rw] = (of, od, cs.clone(), o96, cs96)
+            lgt = torch.empty(B, 3, H, W, device="cuda")
+            hs = torch.empty(B * H * W, 96, device="cuda", dtype=torch.bfloat16)
+            th = timeit(lambda: heads(lgt, hs))
+            outs[rw] = (of, od, cs.clone(), o96, cs96, lgt, hs)
             by_f = B * H * W * 64 * 2 * 2
             by_d = B * H * W * 64 * 2 * 3
             print(f"round {rnd} RW={rw}: fwd {tf * 1e6:8.1f} us ({fl / tf / 1e12:6.1f} TF/s, {by_f / tf / 1e9:6.0f} GB/s) | "
                   f"dgrad {td * 1e6:8.1f} us ({fl / td / 1e12:6.1f} TF/s, {by_d / td / 1e9:6.0f} GB/s) | dgrad 64<-96 {t96 * 1e6:8.1f} us "
-                  f"({fl * 1.5 / t96 / 1e12:6.1f} TF/s, {by_d * 3.5 / 3 / t96 / 1e9:6.0f} GB/s)", flush=True)
-    for i, name in enumerate(("fwd", "dgrad", "colsum", "dgrad 64<-96", "colsum 64<-96")):
+                  f"({fl * 1.5 / t96 / 1e12:6.1f} TF/s, {by_d * 3.5 / 3 / t96 / 1e9:6.0f} GB/s) | heads {th * 1e6:8.1f} us "
+                  f"({fl * 1.5 / th / 1e12:6.1f} TF/s, {B * H * W * (128 + 192 + 12) / th / 1e9:6.0f} GB/s)", flush=True)
+    for i, name in enumerate(("fwd", "dgrad", "colsum", "dgrad 64<-96", "colsum 64<-96", "head logits", "hsave")):
         a, b = outs["0"][i].float(), outs["1"][i].float()
         print(f"{name}: max |rw - igemm| / max|igemm| = {float((a - b).abs().max() / b.abs().max().clamp_min(1e-9)):.3e}")
 
