@@ -950,6 +950,7 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
         float bn_ = bias ? bias[n] : 0.f;
         for (int r = ph; r < BM; r += nph) {
           if (m0 + r >= M) break;
+          if (rm.mode == 3 && rm.map(m0 + r) < 0) continue;     // tile rows outside the image
           float v = ct[r * LDT + c] + bn_;
           s += v; q += v * v;
         }
@@ -1164,6 +1165,187 @@ __global__ void __launch_bounds__(GEMM_THREADS, 1) igemm_pp_kernel(LA la0, LB lb
   }
 }
 constexpr int PP_LDS = 128 * (256 + 4) * 4;   // C chunk (133 KB) >= the two 64 KB K stages
+
+// ------------------------------------------------------------------ halo ping-pong 3x3 conv (bf16)
+// 3x3 / stride 1 / pad 1 NHWC conv, Cin % 64 == 0, Cout % 256 == 0, on the 256x256 ping-pong schedule above,
+// with the A operand (im2col) formed from an input HALO in LDS instead of being gathered per K tile:
+//   * tile = 8 x 32 output pixels (256 virtual rows, RowMap mode 3) x 256 output channels;
+//   * K order = (channel chunk c of 64, tap): step s = 9 c + tap.  Chunk c's (8+2) x (32+2) x 64 halo sits in
+//     one of two LDS images for its 9 steps; every tap reads its A fragments at shifted pixel positions
+//     (per-lane base + immediate: halo row px, 16-B slot = chunk ^ (px & 7), conflict-free for every tap);
+//   * chunk c+1's halo trickles in during steps 9c .. 9c+5 (one 1-KiB LDS-DMA piece per wave per step,
+//     issued BEHIND that step's B halves, so the phase-3 vmcnt that retires the B halves leaves it in
+//     flight and the next step's wait retires it; read from step 9c+9 on);
+//   * B (weights [Cout][9][Cin]) and its buffers as in igemm_pp_kernel, the K-tile index remapped to
+//     tap * Cin/64 + c.  WAR on a halo image: its chunk-(c-1) reads end in phase 1 of step 9c-1, the first
+//     piece of chunk c+1 lands from phase 0 of step 9c (>= 2 phases later, as for the B halves).
+constexpr int HPP_PPW = 6, HPP_HB = 8 * HPP_PPW * 1024;          // 340 px x 128 B = 42.5 KiB -> 48 pieces
+constexpr int HPP_LDS = 2 * HPP_HB + 2 * 2 * 128 * 128;          // 2 halos + 2 x two B half images = 160 KiB
+static_assert(HPP_LDS <= 160 * 1024 && PP_LDS <= HPP_LDS, "halo ping-pong LDS budget");
+
+template <bool RELU, class LB, class EPI>
+__global__ void __launch_bounds__(GEMM_THREADS, 1) conv3x3_hpp_kernel(const bf16* __restrict__ x, LB lb0, EPI epi, int H, int W,
+                                                                       int Cin, int tiles_x, int tiles_y, int flags) {
+  constexpr int BN = 256, HB = 128 * 128, LDT = BN + 4, HC = 34, PX = 340;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int wr = wave >> 2, wc = wave & 3;
+  int m0, n0, tile;
+  {
+    const int nwg = gridDim.x * gridDim.y;
+    const int L = blockIdx.y * gridDim.x + blockIdx.x;
+    const int q = nwg >> 3, r = nwg & 7, xcd = L & 7, idx = L >> 3;
+    const int Wl = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+    tile = Wl / gridDim.x; m0 = tile * 256; n0 = (Wl % gridDim.x) * BN;
+  }
+  const int txi = tile % tiles_x, t2 = tile / tiles_x, tyi = t2 % tiles_y, bb = t2 / tiles_y;
+  const int nch = Cin >> 6, nt = 9 * nch;
+  epi.prepare(0);
+  LB lb1 = lb0;
+  lb0.setup(n0, tid); lb1.setup(n0 + 128, tid);
+  char* Bb = smem + 2 * HPP_HB;                    // B buffer of step s: Bb + (s & 1) * 2 HB
+  const bool stag = !(flags & 1);
+  // halo DMA: piece p = 6 wave + i covers bytes [1024 p, +1024) of a halo image.  Everything is recomputed per
+  // piece from an opaque (scalar) i: one piece per wave per step, and any per-i value kept live across the chunk
+  // loop spills (the ping-pong body owns ~240 registers), whose reload's vmcnt(0) would serialise the DMA
+  const long img = (long)H * W * Cin;
+  const auto rx = make_rsrc(x + bb * img, (unsigned long)img * 2);
+  const int ty0 = tyi * 8 - 1, tx0 = txi * 32 - 1;
+  auto halo_piece = [&](int c, int i0, char* himg) {
+    int i = i0;
+    asm volatile("" : "+s"(i));
+    const int b = (wave * HPP_PPW + i) * 1024 + lane * 16, px = b >> 7, ch = ((b >> 4) & 7) ^ (px & 7);
+    const int hy = px / HC, gy = ty0 + hy, gx = tx0 + (px - hy * HC);
+    const bool ok = px < PX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+    blds16(rx, ok ? (unsigned)(((gy * W + gx) * Cin + c * 64) * 2 + ch * 16) : BUF_OOB, himg + (wave * HPP_PPW + i) * 1024);
+  };
+  // A fragment of block (qm, i), k-half kk, tap (dy, dx): halo px = Lw + off, Lw = 136 wr + (lane & 15),
+  // off = (2 qm + (i >> 1) + dy) * 34 + 16 (i & 1) + dx (compile-time).  Byte = 128 px + 16 (chunk ^ (px & 7)):
+  // the slot term of kk = 0 depends on the lane and on off & 7 only -> 8 per-lane bytes 16 (g ^ ((Lw + j) & 7))
+  // packed four to a register (ysl); kk = 1 reads chunk 4 + g = g ^ 4 -> the byte ^ 64
+  const int Lw = 4 * HC * wr + (lane & 15), yb0 = Lw * 128;
+  unsigned ysl[2] = {0u, 0u};
+  {
+    const int g = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < 8; j++) ysl[j >> 2] |= (unsigned)(16 * (g ^ ((Lw + j) & 7))) << (8 * (j & 3));
+  }
+  PPFrag<LB::KCL> pfb; pfb.init(lane, wc & 1);
+  const int boff = LB::KCL ? (wc & 1) * 64 * 128 : 0;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+#pragma unroll
+    for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // one set of A fragments: the halo stays resident for the chunk, so quadrant row qm = 1 is read in phase 2
+  // (after qm = 0's last use) instead of beside qm = 0 as in igemm_pp_kernel (32 registers fewer)
+  bf16x8 fa[4][2], fb[2][2][2];
+  auto rdA = [&](const char* Hc, auto TAP, int qm) {
+    constexpr int tap = decltype(TAP)::value, dy = tap / 3, dx = tap % 3;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int kk = 0; kk < 2; kk++) {
+        const int off = (2 * qm + (i >> 1) + dy) * HC + 16 * (i & 1) + dx;
+        const int j = off & 7, sl = (int)__builtin_amdgcn_ubfe(ysl[j >> 2], 8 * (j & 3), 8);
+        fa[i][kk] = *(const bf16x8*)(Hc + yb0 + (kk ? (sl ^ 64) : sl) + off * 128);
+      }
+  };
+  auto rdB = [&](const char* Bs, int qn) {
+#pragma unroll
+    for (int j = 0; j < 2; j++)
+#pragma unroll
+      for (int kk = 0; kk < 2; kk++) fb[qn][j][kk] = pfb.read(Bs, qn * 32 + j * 16, kk);
+  };
+  // sched_barrier(0) pins each phase's 16 MFMAs between its two barriers: with the 9 taps unrolled the scheduler
+  // would otherwise sink them below the next phase's LDS reads (destroying the compute / load alternation)
+  auto mm = [&](int qm, int qn) {
+    raw_barrier();
+    wait_lgkm0();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+          acc[qm * 4 + i][qn * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[qn][j][kk], fa[i][kk], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    raw_barrier();
+  };
+  auto kv = [&](int s) { return (s % 9) * nch + s / 9; };     // B K tile of step s
+  // RELU (the ReLU'd input of an RCU's first conv): applied once per halo in LDS instead of per fragment read;
+  // each wave rewrites the pieces it DMA'd itself, after its own vmcnt wait retired them
+  auto relu_own = [&](char* himg) {
+#pragma unroll 1
+    for (int i = 0; i < HPP_PPW; i++) {
+      bf16x8* q = (bf16x8*)(himg + (wave * HPP_PPW + i) * 1024 + lane * 16);
+      *q = relu_frag(*q);
+    }
+  };
+  // prologue: the whole halo of chunk 0, the B halves of step 0
+#pragma unroll
+  for (int i = 0; i < HPP_PPW; i++) halo_piece(0, i, smem);
+  lb0.issue(kv(0), Bb); lb1.issue(kv(0), Bb + HB);
+  wait_vmcnt<0>();
+  if constexpr (RELU) { relu_own(smem); wait_lgkm0(); }
+  raw_barrier();
+  if (wr && stag) raw_barrier();                   // stagger: the wr = 1 half runs one barrier behind
+  for (int c = 0; c < nch; c++) {
+    const char* Hc = smem + (c & 1) * HPP_HB;
+    char* Hn = smem + ((c + 1) & 1) * HPP_HB;
+    const bool nxt = c + 1 < nch;
+    auto step = [&](auto TAP) {
+      constexpr int tap = decltype(TAP)::value;
+      // keep the fragment addresses per step (otherwise all 9 x 16 are hoisted out of the chunk loop and spill)
+      asm volatile("" : "+v"(ysl[0]), "+v"(ysl[1]));
+#pragma unroll
+      for (int i = 0; i < LB::NIW; i++) { asm volatile("" : "+v"(lb0.vo[i])); asm volatile("" : "+v"(lb1.vo[i])); }
+      const int s = 9 * c + tap;
+      const char* Bs = Bb + (s & 1) * 2 * HB + (wc >> 1) * HB + boff;
+      char* Bn = Bb + ((s + 1) & 1) * 2 * HB;
+      const bool more = s + 1 < nt;
+      // phase 0: quadrant (0,0); B halves of step s+1, then (taps 0-5) one halo piece of chunk c+1
+      rdA(Hc, TAP, 0); rdB(Bs, 0);
+      if (more) { lb0.issue(kv(s + 1), Bn); lb1.issue(kv(s + 1), Bn + HB); }
+      if (tap < HPP_PPW && nxt) halo_piece(c + 1, tap, Hn);
+      if constexpr (RELU && tap == 7) { if (nxt) relu_own(Hn); }   // its pieces were retired in step 9c+6
+      mm(0, 0);
+      // phase 1: quadrant (0,1); the step's last B reads
+      rdB(Bs, 1);
+      mm(0, 1);
+      // phase 2: quadrant (1,1); A rows of quadrant row 1
+      rdA(Hc, TAP, 1);
+      mm(1, 1);
+      // phase 3: quadrant (1,0); retire the B halves of step s+1 (this step's halo piece stays in flight)
+      if (more) { if (tap < HPP_PPW && nxt) wait_vmcnt<1>(); else wait_vmcnt<0>(); }
+      mm(1, 0);
+    };
+    step(std::integral_constant<int, 0>{}); step(std::integral_constant<int, 1>{}); step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 3>{}); step(std::integral_constant<int, 4>{}); step(std::integral_constant<int, 5>{});
+    step(std::integral_constant<int, 6>{}); step(std::integral_constant<int, 7>{}); step(std::integral_constant<int, 8>{});
+  }
+  if (!wr && stag) raw_barrier();                  // re-align the two halves
+  float* ct = (float*)smem;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    lds_barrier();
+    if (wr == h) {
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int r = i * 16 + (lane & 15), col = wc * 64 + j * 16 + (lane >> 4) * 4;
+          *(f32x4*)(ct + r * LDT + col) = acc[i][j];
+        }
+    }
+    lds_barrier();
+    epi(ct, LDT, m0 + h * 128, n0, tid, 128, BN, GEMM_THREADS);
+  }
+}
 
 // WM_: waves along M (0 = by tile shape); e.g. 512x64 tiles use WM_=8 for 64x64 per-wave tiles
 template <typename T, int BM, int BN, class LA, class LB, class EPI, int NST = 3, int WM_ = 0>

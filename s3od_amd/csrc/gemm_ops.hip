@@ -630,6 +630,38 @@ static int launch_rw(const bf16* x, const bf16* w, const float* bias, const bf16
   return s3od_check_launch("conv3x3_c64_rw");
 }
 
+// ---------------------------------------------------------------- halo ping-pong 3x3 conv launcher
+// For 3x3 s1 bf16 convs with Cin % 64 == 0, Cout % 256 == 0 and at least two rounds of 256 tiles (the RCU /
+// layer_rn convs at 256^2 .. 128^2 maps).  OFF by default: measured slower than the 128x128 implicit GEMM
+// (tools/conv256_bench.py, bs 16, relu_in + bias + BN sums: 256^2 2.06 vs 1.72 ms, 128^2 0.55 vs 0.46 ms):
+// the 160 KiB of LDS (two halos + two B stages) leaves the B halves and the trickled halo pieces only one step
+// of latency cover, and in-order vmcnt makes every step's B wait also wait for the previous step's HBM halo
+// piece.  S3OD_CONV_HPP=1 enables it (auto), =2 forces it on any map (read per call: A/B and tests).
+static bool hpp_ok(int dtype, int B, int H, int W, int Cin, int Cout) {
+  const char* e = getenv("S3OD_CONV_HPP");
+  const int knob = e ? atoi(e) : 0;               // 0 off (default), 1 auto, 2 forced (tests: small maps)
+  if (knob == 0) return false;
+  const long tiles = (long)B * cdiv(H, HT_TH) * cdiv(W, HT_TW) * (Cout / 256);
+  return dtype == S3OD_BF16 && Cin % 64 == 0 && Cout % 256 == 0 && (tiles >= 512 || knob == 2) &&
+         (unsigned long)H * W * Cin * 2 < BUF_MAX && (long)H * W * Cin < (1L << 30);
+}
+template <class EPI>
+static int launch_hpp(const bf16* x, const bf16* wp, int relu_in, EPI e, int B, int H, int W, int Cin, int Cout, hipStream_t st) {
+  const int K = 9 * Cin, tx = cdiv(W, HT_TW), ty = cdiv(H, HT_TH);
+  DenseKC<bf16, 128> lb{wp, (long)K, Cout, K, 0};
+  if (!lb.buf_ok()) { s3od_set_error("conv hpp: weight window too large"); return 22; }
+  static const int flags = dev_knob("S3OD_PP_FLAGS", 0);
+  dim3 grid(Cout / 256, B * tx * ty);
+  auto go = [&](auto kfn) {
+    static bool attr = false;
+    if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, HPP_LDS); attr = true; }
+    hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), HPP_LDS, st, x, lb, e, H, W, Cin, tx, ty, flags);
+  };
+  if (relu_in) go(conv3x3_hpp_kernel<true, decltype(lb), EPI>);
+  else go(conv3x3_hpp_kernel<false, decltype(lb), EPI>);
+  return s3od_check_launch("conv3x3_hpp");
+}
+
 // ---------------------------------------------------------------- halo-tile 3x3 weight gradient
 // dW[co][tap][ci] = sum_px dy[px][co] * x[px + tap][ci] for a 3x3 / stride 1 / pad 1 conv with Cin = 64
 // and Cout = 64 / 96 (the full-resolution decoder convs).  The implicit-GEMM wgrad tiles N = 9*64 into
@@ -956,6 +988,13 @@ int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int C
       !scale && !shift && !res1 && !res2 && !pre && !colsum && (act == ACT_NONE || act == ACT_RELU) && rw_ok(dtype, B, H, W))
     return act == ACT_RELU ? launch_rw<2, 64>((const bf16*)x, (const bf16*)wp, bias, nullptr, nullptr, (bf16*)out, B, H, W, st)
                            : launch_rw<0, 64>((const bf16*)x, (const bf16*)wp, bias, nullptr, nullptr, (bf16*)out, B, H, W, st);
+  if (KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && hpp_ok(dtype, B, H, W, Cin, Cout)) {
+    RowMap rm = halo_rowmap(H, W);
+    const int Mv = B * rm.RH * rm.RW * HT_TH * HT_TW;
+    EpiStd<bf16, bf16> e{(bf16*)out, (long)Cout, 0, bias, scale, shift, (const bf16*)res1, (long)Cout, (const bf16*)res2, (long)Cout,
+                         (bf16*)pre, (long)Cout, stats, act, Mv, N, rm, colsum};
+    return launch_hpp((const bf16*)x, (const bf16*)wp, relu_in, e, B, H, W, Cin, Cout, st);
+  }
   if (KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && !relu_in && !stats && Cout == 64 && halo_ok(dtype, Cin, Cout)) {
     RowMap rm = halo_rowmap(H, W);
     const int Mv = B * rm.RH * rm.RW * HT_TH * HT_TW;
