@@ -10,24 +10,29 @@ on the GPU with one fused HIP launch per sample (``s3od_augment_sample``, data_o
 
 * mode "test": LongestMaxSize(S) + centred PadIfNeeded(S, fill 0) + Normalize (transforms.py:14-28);
 * mode "regular": + HorizontalFlip 0.5, VerticalFlip 0.2, RandomRotate90 0.2, RandomResizedCrop
-  0.5 (scale 0.85-1, ratio 0.9-1.1), Rotate ±15° 0.2 (composed into one affine map), ColorJitter
-  (brightness 0.5, contrast 0.5, saturation 0.2, hue 0.2; p 0.7 inside OneOf p 0.5), noise OneOf
-  p 0.3 of Gaussian (std 0.2-0.44) / multiplicative (0.9-1.1) (transforms.py:30-71);
+  0.5 (scale 0.85-1, ratio 0.9-1.1), Rotate ±15° 0.2 (composed into one affine map), OneOf p 0.5 of
+  ColorJitter (brightness 0.5, contrast 0.5, saturation 0.2, hue 0.2; weight 0.7) / Sharpen (alpha
+  0.2-0.5, lightness 0.5-1.0; weight 0.3), noise OneOf p 0.3 of Gaussian (std 0.2-0.44) / ISONoise
+  (colour shift 0.01-0.05, intensity 0.1-0.5; HLS + Poisson) / multiplicative (0.9-1.1)
+  (transforms.py:30-71).  A draw of Sharpen or ISONoise runs the two-stage chain of
+  ``s3od_augment_synthetic`` (order 1) after the geometry pass;
 * mode "synthetic" (transforms.py:65-220): the "regular" geometry + the synthetic groups, each a
   OneOf with the reference's probabilities and member weights: colour (ColorJitter 0.4/0.4/0.3/0.2 |
-  HueSaturationValue 25/35/30 | CLAHE*), noise (ISONoise | GaussNoise 0.25-0.6 | MultiplicativeNoise),
-  quality (ImageCompression* | Downscale 0.4-0.7), lighting (RandomShadow 1-3 | RandomBrightnessContrast
-  0.4/0.4), blur (MotionBlur | GaussianBlur 3-7 | Defocus 2-6 | ZoomBlur*), colour space (ToSepia |
-  ToGray | ChannelShuffle, p 0.05), distortion (OpticalDistortion 0.3 | GridDistortion* |
-  ElasticTransform* | Perspective 0.05-0.1, geometry also applied to the mask), detail (Emboss |
-  Sharpen | Posterize 5 bits) and weather (RandomSnow* | RandomRain*, p 0.15).  Members marked * are
-  not built: when the OneOf draws one of them the group is a no-op.  Three HIP passes per sample:
-  geometry -> raw [0,1] RGB, per-pixel photometric chain, then one composed (blur * sharpen/emboss)
-  filter with the Downscale sampling, colour space, posterize and Normalize (s3od_augment_synthetic).
+  HueSaturationValue 25/35/30 | CLAHE 4.0 / 8x8 tiles), noise (ISONoise | GaussNoise 0.25-0.6 |
+  MultiplicativeNoise), quality (ImageCompression 50-95: 8x8 DCT, 4:2:0 chroma, libjpeg tables |
+  Downscale 0.4-0.7), lighting (RandomShadow 1-3 pentagons | RandomBrightnessContrast 0.4/0.4), blur
+  (MotionBlur | GaussianBlur 3-7 | Defocus 2-6 | ZoomBlur 1-1.1), colour space (ToSepia | ToGray |
+  ChannelShuffle, p 0.05), distortion (OpticalDistortion 0.3 | GridDistortion 6 steps | ElasticTransform |
+  Perspective 0.05-0.1, geometry also applied to the mask), detail (Emboss | Sharpen | Posterize 5 bits)
+  and weather (RandomSnow | RandomRain, p 0.15).  Three HIP passes per sample: geometry + distortion ->
+  raw [0,1] RGB, the per-pixel photometric chain (with the CLAHE / JPEG / ZoomBlur / rain / snow
+  stages), then one composed (blur * sharpen/emboss) filter with the Downscale sampling, colour space,
+  posterize and Normalize (s3od_augment_synthetic).
 
 albumentations / cv2 are not in this image, so the augmentations follow the published semantics
-of those transforms but are NOT bit-matched to them ("parity unpinned"); the "test" mode is
-checked against a numpy restatement in tests/test_gpu_data.py.
+of albumentations 2.0.8 but are NOT bit-matched to it ("parity unpinned"); every member is checked
+against the numpy restatement in oracle/augment_oracle.py (tests/test_gpu_augment.py, JPEG pinned
+to libjpeg through PIL) and the "test" mode against tests/test_gpu_data.py.
 """
 from __future__ import annotations
 
