@@ -11,6 +11,8 @@
   } while (0)
 
 static RowMap dense_rm() { RowMap r{}; r.mode = 0; return r; }
+// a per-call dev switch: true when the variable is set to 0 (A/B inside one process)
+static bool getenv_zero(const char* n) { const char* e = getenv(n); return e && atoi(e) == 0; }
 
 // Tile configuration (dev knob for the micro-benchmarks): S3OD_GEMM_CFG=<n> forces one config for
 // every GEMM entry point; default (-1) = per-op choice below.
@@ -972,6 +974,40 @@ int s3od_qkv_rope_fwd(int dtype, int B, int Ntok, int P, int H, const void* x, c
   return 0;
 }
 
+// implicit-GEMM conv forward (im2col gathered per K tile by ConvFwdA); also the stride-1 3x3 data gradient run as a
+// forward conv of dy with the transposed, tap-reversed weight (s3od_conv_dgrad with wT)
+static int conv_fwd_igemm(int dtype, ConvGeo g, int M, int N, int K, int Cin, int Cout, const void* x, int relu_in,
+                          const void* wp, const float* bias, const float* scale, const float* shift, int act,
+                          const void* res1, const void* res2, void* out, void* pre, double* stats, float* colsum,
+                          hipStream_t st) {
+  DISPATCH_T(dtype, {
+    const int KTILES = cdiv(K, KT<T>::BK);
+    auto go = [&](auto bn, auto rl) -> int {
+      return with_cfg<T>(Cout <= 64 ? 3 : 1, [&](auto C0) -> int {
+        typedef ConvCfg<decltype(C0), decltype(bn)::value> CC;
+        constexpr int BM = CC::BM, NST = CC::NST;
+        constexpr int BN = decltype(bn)::value < CC::BN ? decltype(bn)::value : CC::BN;
+        constexpr int LN = CC::PP ? CC::LN : BN;
+        CC C{};
+        ConvFwdA<T, CC::LM, decltype(rl)::value, CC::W> la{}; la.x = (const T*)x; la.g = g; la.M = M; la.relu = relu_in;
+        DenseKC<T, LN, CC::W> lb{(const T*)wp, (long)K, N, K, 0};
+        EpiStd<T, T> e{(T*)out, (long)Cout, 0, bias, scale, shift, (const T*)res1, (long)Cout, (const T*)res2, (long)Cout,
+                       (T*)pre, (long)Cout, stats, act, M, N, dense_rm(), colsum};
+        return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, M, N, KTILES, 1, 1, st);
+      });
+    };
+    if (relu_in) {
+      if (Cout <= 64) return go(std::integral_constant<int, 64>{}, std::true_type{});
+      if (Cout < 256) return go(std::integral_constant<int, 128>{}, std::true_type{});
+      return go(std::integral_constant<int, 256>{}, std::true_type{});
+    }
+    if (Cout <= 64) return go(std::integral_constant<int, 64>{}, std::false_type{});
+    if (Cout < 256) return go(std::integral_constant<int, 128>{}, std::false_type{});
+    return go(std::integral_constant<int, 256>{}, std::false_type{});
+  });
+  return 0;
+}
+
 // ---------------------------------------------------------------------------------- convs
 // NHWC activations, weights repacked [Cout][KH][KW][Cin].
 // pre = conv(relu?(x)) + bias[n]; out[b,oy,ox,n] = act(pre*scale[n] + shift[n]) (+res1 +res2);
@@ -1002,32 +1038,8 @@ int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int C
                          (bf16*)pre, (long)Cout, nullptr, act, Mv, N, rm, colsum};
     return launch_halo<64>((const bf16*)x, (const bf16*)wp, e, B, H, W, st);
   }
-  DISPATCH_T(dtype, {
-    const int KTILES = cdiv(K, KT<T>::BK);
-    auto go = [&](auto bn, auto rl) -> int {
-      return with_cfg<T>(Cout <= 64 ? 3 : 1, [&](auto C0) -> int {
-        typedef ConvCfg<decltype(C0), decltype(bn)::value> CC;
-        constexpr int BM = CC::BM, NST = CC::NST;
-        constexpr int BN = decltype(bn)::value < CC::BN ? decltype(bn)::value : CC::BN;
-        constexpr int LN = CC::PP ? CC::LN : BN;
-        CC C{};
-        ConvFwdA<T, CC::LM, decltype(rl)::value, CC::W> la{}; la.x = (const T*)x; la.g = g; la.M = M; la.relu = relu_in;
-        DenseKC<T, LN, CC::W> lb{(const T*)wp, (long)K, N, K, 0};
-        EpiStd<T, T> e{(T*)out, (long)Cout, 0, bias, scale, shift, (const T*)res1, (long)Cout, (const T*)res2, (long)Cout,
-                       (T*)pre, (long)Cout, stats, act, M, N, dense_rm(), colsum};
-        return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, M, N, KTILES, 1, 1, st);
-      });
-    };
-    if (relu_in) {
-      if (Cout <= 64) return go(std::integral_constant<int, 64>{}, std::true_type{});
-      if (Cout < 256) return go(std::integral_constant<int, 128>{}, std::true_type{});
-      return go(std::integral_constant<int, 256>{}, std::true_type{});
-    }
-    if (Cout <= 64) return go(std::integral_constant<int, 64>{}, std::false_type{});
-    if (Cout < 256) return go(std::integral_constant<int, 128>{}, std::false_type{});
-    return go(std::integral_constant<int, 256>{}, std::false_type{});
-  });
-  return 0;
+  return conv_fwd_igemm(dtype, g, M, N, K, Cin, Cout, x, relu_in, wp, bias, scale, shift, act, res1, res2, out, pre, stats,
+                        colsum, st);
 }
 
 // conv dgrad == ConvTranspose2d forward.  dy: [B,OH,OW,Cout] (conv output grid); w: [Cout][KH][KW][Cin];
@@ -1044,6 +1056,14 @@ int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
                                          W, (hipStream_t)stream)
                       : launch_rw<1, 96>((const bf16*)dy, (const bf16*)wT, nullptr, (const bf16*)res1, colsum, (bf16*)dx, B, H,
                                          W, (hipStream_t)stream);
+  if (wT && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && (Cin != 64 || Cout > 96) && !pre &&
+      !stats && !getenv_zero("S3OD_DGRAD_WT")) {
+    // stride-1 3x3 data gradient = forward conv of dy (Cout channels) with wT [Cin][3][3][Cout]: the forward
+    // gather (ConvFwdA) instead of the transposed-conv gather (measured faster on the 256-channel RCU convs)
+    ConvGeo gf{}; gf.B = B; gf.SH = H; gf.SW = W; gf.SC = Cout; gf.RH = H; gf.RW = W; gf.KH = 3; gf.KW = 3; gf.s = 1; gf.p = 1;
+    return conv_fwd_igemm(dtype, gf, B * H * W, Cin, 9 * Cout, Cout, Cin, dy, 0, wT, bias, scale, shift, act, res1, res2, dx,
+                          nullptr, nullptr, colsum, (hipStream_t)stream);
+  }
   if (wT && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && !stats && Cin == 64 && Cout == 64 &&
       halo_ok(dtype, Cout, Cin)) {
     // stride-1 3x3 data gradient = forward conv of dy with the transposed, tap-reversed weight wT

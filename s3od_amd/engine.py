@@ -157,7 +157,19 @@ class DPTEngine:
         for k in range(nm):
             pack(m + f"mask_heads.{k}.0.weight", 32, 64, 3, 3, dst=heads, off=k * 32 * 9 * 64)
         w["heads1"] = heads
-        if self.dt == BF16:       # data-gradient weights of the halo-tile conv path (bf16 only)
+        if self.dt == BF16:       # data-gradient weights of the 3x3 s1 convs, run as forward convs (bf16 only)
+            for r in (1, 2, 3, 4):
+                q = h + f"scratch.refinenet{r}."
+                for u in (1, 2):
+                    for cv in (1, 2):
+                        key = f"ref{r}.u{u}.c{cv}T"
+                        w[key] = torch.empty((256, 3, 3, 256), dtype=T, device=dev)
+                        pack_dgrad(q + f"resConfUnit{u}.conv{cv}.weight", 256, 256, w[key], 0, 256)
+            for i, c in enumerate(OUT_CH):
+                w[f"rn{i + 1}T"] = torch.empty((c, 3, 3, 256), dtype=T, device=dev)
+                pack_dgrad(h + f"scratch.layer{i + 1}_rn.weight", 256, c, w[f"rn{i + 1}T"], 0, 256)
+            w["oc1T"] = torch.empty((256, 3, 3, 128), dtype=T, device=dev)
+            pack_dgrad(m + "output_conv1.weight", 128, 256, w["oc1T"], 0, 128)
             w["c64T"] = torch.empty((64, 3, 3, 64), dtype=T, device=dev)
             pack_dgrad(m + "upsample_2x.2.weight", 64, 64, w["c64T"], 0, 64)
             w["heads1T"] = torch.empty((64, 3, 3, 32 * nm), dtype=T, device=dev)
@@ -438,11 +450,11 @@ class DPTEngine:
               None, out, None, None, colsum, wT, stream())
         return out
 
-    def _dgrad_conv_res(self, dy, w, B, H, W, C, act, res1, res2):
+    def _dgrad_conv_res(self, dy, w, B, H, W, C, act, res1, res2, wT=None):
         """3x3 s1 dgrad with RELU_BWD mask (res1 = the un-ReLU'd input) plus a residual gradient res2."""
         out = torch.empty((B, H, W, C), dtype=self.tdt, device=dy.device)
         lib()("s3od_conv_dgrad", self.dt, B, H, W, C, H, W, C, 3, 3, 1, 1, dy, w, None, None, None, act, res1,
-              res2, out, None, None, None, None, stream())
+              res2, out, None, None, None, wT, stream())
         return out
 
     def _rcu_bwd(self, d_out, r, u, B, ctx, G):
@@ -460,14 +472,14 @@ class DPTEngine:
         L("s3od_bn_bwd", self.dt, d_out, c["z2"], None, c["bn2"]["mean"], c["bn2"]["rstd"], P[q + "bn2.weight"], sums, dz2,
           G[q + "bn2.weight"], G[q + "bn2.bias"], G[q + "conv2.bias"], npix, 256, st)
         self._wgrad_conv(dz2, c["a1"], B, h, w, 256, h, w, 256, 3, 1, 1, G[q + "conv2.weight"])
-        da1 = self._dgrad_conv(dz2, W8[tag + ".c2"], B, h, w, 256, h, w, 256, 3, 1, 1)
+        da1 = self._dgrad_conv(dz2, W8[tag + ".c2"], B, h, w, 256, h, w, 256, 3, 1, 1, wT=W8.get(tag + ".c2T"))
         dz1 = torch.empty_like(d_out)
         # ReLU mask recomputed from z1 and bn1's scale/shift (bit-identical to a1 > 0): a1 is not read
         L("s3od_bn_relu_bwd", self.dt, da1, c["z1"], c["bn1"]["scale"], c["bn1"]["shift"], c["bn1"]["mean"],
           c["bn1"]["rstd"], P[q + "bn1.weight"], sums, dz1,
           G[q + "bn1.weight"], G[q + "bn1.bias"], G[q + "conv1.bias"], npix, 256, st)
         self._wgrad_conv(dz1, c["x"], B, h, w, 256, h, w, 256, 3, 1, 1, G[q + "conv1.weight"], relu_x=True)
-        return self._dgrad_conv_res(dz1, W8[tag + ".c1"], B, h, w, 256, ACT_RELU_BWD, c["x"], d_out)
+        return self._dgrad_conv_res(dz1, W8[tag + ".c1"], B, h, w, 256, ACT_RELU_BWD, c["x"], d_out, wT=W8.get(tag + ".c1T"))
 
     def _fusion_bwd(self, r, d_p, B, ctx, G, bcast=None, two_inputs=True):
         """Backward of FeatureFusionBlock r. Returns (d_x0, d_x1) (d_x1 None for refinenet4)."""
@@ -520,7 +532,7 @@ class DPTEngine:
         doc1 = self._conv(dup, W8["up2x"], B, HH, WW, 64, 128, 4, 2, 1, colsum=G[m + "output_conv1.bias"])
         # ---- output_conv1 3x3 256->128
         self._wgrad_conv(doc1, p1, B, H1, W1, 256, H1, W1, 128, 3, 1, 1, G[m + "output_conv1.weight"])
-        dp1 = self._dgrad_conv(doc1, W8["oc1"], B, H1, W1, 256, H1, W1, 128, 3, 1, 1)
+        dp1 = self._dgrad_conv(doc1, W8["oc1"], B, H1, W1, 256, H1, W1, 128, 3, 1, 1, wT=W8.get("oc1T"))
         if d_feat is not None:     # gradient of the returned features (= path_1, NCHW view)
             dp1.add_(d_feat.permute(0, 2, 3, 1).to(dp1.dtype))
         # ---- classifier head -> broadcast gradient onto path_1 (folded into the bilinear backward)
@@ -543,7 +555,8 @@ class DPTEngine:
             hh, ww = dims[i]
             C = f.shape[3]
             self._wgrad_conv(drn[i], f, B, hh, ww, C, hh, ww, 256, 3, 1, 1, G[h + f"scratch.layer{i + 1}_rn.weight"])
-            dfeat.append(self._dgrad_conv(drn[i], W8[f"rn{i + 1}"], B, hh, ww, C, hh, ww, 256, 3, 1, 1, colsum=G[fbias[i]]))
+            dfeat.append(self._dgrad_conv(drn[i], W8[f"rn{i + 1}"], B, hh, ww, C, hh, ww, 256, 3, 1, 1, colsum=G[fbias[i]],
+                                          wT=W8.get(f"rn{i + 1}T")))
         proj = dec["proj"]
         dproj = [None] * 4
         # resize0: ConvT 256 k4 s4 (conv view: Y = proj0 grid, X = f0 grid)

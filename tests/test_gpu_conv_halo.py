@@ -121,3 +121,29 @@ def test_conv_wgrad_halo_channel_blocks(cin, cout, B, H, W, relu):
     torch.cuda.synchronize()
     assert int((ws != 0).sum()) == 0, "conv_wgrad must leave its workspace all zero"
     assert float((dw - ref).abs().max() / ref.abs().max()) < 2e-3, float((dw - ref).abs().max() / ref.abs().max())
+
+
+@pytest.mark.parametrize("cin,cout,H,W", [(256, 256, 40, 70), (512, 256, 33, 20), (256, 128, 24, 40)])
+def test_conv_dgrad_via_transposed_weight(cin, cout, H, W):
+    """3x3 s1 data gradient run as a forward conv of dy with wT = the transposed, tap-reversed weight (the RCU /
+    layerK_rn / output_conv1 path, bf16): ReLU' mask of res1, the residual gradient res2 and the bias column sums,
+    vs fp32 conv_transpose2d of the same bf16 operands."""
+    from s3od_amd._lib import lib, stream
+    B = 2
+    g = torch.Generator(device="cuda").manual_seed(cin + cout + H)
+    dy = torch.randn(B, cout, H, W, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(cout, cin, 3, 3, device="cuda", generator=g) * (1.0 / (3 * cout ** 0.5))).bfloat16()
+    res1 = torch.randn(B, cin, H, W, device="cuda", generator=g).bfloat16()
+    res2 = torch.randn(B, cin, H, W, device="cuda", generator=g).bfloat16()
+    dx_ref = F.conv_transpose2d(dy.float(), w.float(), padding=1) * (res1.float() > 0)
+    ref = dx_ref + res2.float()
+    wp = w.permute(0, 2, 3, 1).contiguous()                                            # [Cout][3][3][Cin]
+    wT = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()                                 # [Cin][3][3][Cout]
+    dx = torch.empty(B, H, W, cin, device="cuda", dtype=torch.bfloat16)
+    cs = torch.zeros(cin, device="cuda")
+    lib()("s3od_conv_dgrad", BF16, B, H, W, cin, H, W, cout, 3, 3, 1, 1, _nhwc(dy), wp, None, None, None, ACT_RELU_BWD,
+          _nhwc(res1), _nhwc(res2), dx, None, None, cs, wT, stream())
+    _close(dx, _nhwc(ref))
+    ref_cs = ref.sum((0, 2, 3))
+    tol = 2e-3 * ref.abs().sum((0, 2, 3)).max()
+    assert float((cs - ref_cs).abs().max()) <= float(tol), (float((cs - ref_cs).abs().max()), float(tol))
