@@ -203,6 +203,65 @@ template <typename T, int R, int NW = GEMM_WAVES> struct DenseKC {          // X
   }
 };
 
+// LayerNorm fused into a GEMM's A operand (north_star "fused LayerNorm+QKV projection", measurement
+// prototype): A[row][k] = bf16((x[row][k] - mean[row]) * rstd[row] * g[k] + b[k]) from the fp32 residual
+// stream, REGISTER staged (LDS-DMA cannot transform): issue_regs loads this lane's 8 fp32 of each chunk,
+// commit normalises them and writes the bf16 chunk to the same LDS position the DMA path would.
+template <int R, int NW = GEMM_WAVES> struct LnA {
+  static constexpr int ROWS = R;
+  static constexpr bool KCL = true, RELU = false, REG = true;
+  typedef KCGeom<bf16, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
+  const float* x; long ld; int nrows, K;
+  const float* mean; const float* rstd; const float* g; const float* b;
+  const float* xb; unsigned long nb;
+  unsigned vo[NIW]; int kel[NIW]; float mu[NIW], rs[NIW];
+  HD bool buf_ok() const { return ((unsigned long)(R - 1) * ld + K) * 4 < BUF_MAX; }
+  DEV void setup(int t0, int tid) {
+    const int lane = tid & 63, wave = wave_id();
+    const int rem = nrows - t0;
+    xb = x + (long)t0 * ld;
+    nb = rem > 0 ? ((unsigned long)(min(rem, R) - 1) * ld + K) * 4 : 0;
+#pragma unroll
+    for (int i = 0; i < NIW; i++) {
+      const int r = G::row(wave, i, lane);
+      kel[i] = G::kel(wave, i, lane);
+      vo[i] = r < rem ? (unsigned)(((long)r * ld + kel[i]) * 4) : BUF_OOB;
+      mu[i] = r < rem ? mean[t0 + r] : 0.f;
+      rs[i] = r < rem ? rstd[t0 + r] : 0.f;
+    }
+  }
+  DEV void issue(int, char*) {}                    // (register-staged only)
+  DEV void issue_regs(int kt, u32x4_t* regs) {     // 2 x 16 B of fp32 per chunk
+    const auto rs_ = make_rsrc(xb, nb);
+    const unsigned adv = (unsigned)(kt * BK * 4);
+#pragma unroll
+    for (int i = 0; i < NIW; i++) {
+      regs[2 * i] = __builtin_amdgcn_raw_buffer_load_b128(rs_, vo[i] + adv, 0, 0);
+      regs[2 * i + 1] = __builtin_amdgcn_raw_buffer_load_b128(rs_, vo[i] + adv + 16, 0, 0);
+    }
+  }
+  DEV void commit(char* tile, const u32x4_t* regs, int kt) const {
+    char* base = tile + wave_id() * NIW * 1024 + (threadIdx.x & 63) * 16;
+#pragma unroll
+    for (int i = 0; i < NIW; i++) {
+      const int k = kt * BK + kel[i];
+      const float4 g0 = *(const float4*)(g + k), g1 = *(const float4*)(g + k + 4);
+      const float4 b0 = *(const float4*)(b + k), b1 = *(const float4*)(b + k + 4);
+      const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        const float xv = __uint_as_float(regs[2 * i + (e >> 2)][e & 3]);
+        o[e] = (bf16)((xv - mu[i]) * rs[i] * gv[e] + bv[e]);
+      }
+      *(bf16x8*)(base + i * 1024) = o;
+    }
+  }
+};
+template <class L> struct IsReg { static constexpr bool v = false; };
+template <int R, int NW> struct IsReg<LnA<R, NW>> { static constexpr bool v = true; };
+
 template <typename T, int R, int NW = GEMM_WAVES> struct DenseMC {          // X[k*ld + col]
   static constexpr int ROWS = R;
   static constexpr bool KCL = false, RELU = false;
@@ -727,13 +786,20 @@ __global__ void __launch_bounds__(GEMM_THREADS) igemm_kernel(LA la, LB lb, EPI e
 
   const int nt = kt1 - kt0;
   constexpr int PD = NST - 1;                 // LDS-DMA prefetch distance (tiles in flight)
+  constexpr bool REGA = IsReg<LA>::v;         // A register staged (transforming loader, 2 stages only)
+  static_assert(!REGA || NST == 2, "register-staged A needs 2 stages");
+  u32x4_t areg[REGA ? 2 * LA::NIW : 1];
   if (nt > 0) {
     // prologue: tiles 0 .. PD-1
 #pragma unroll
     for (int q = 0; q < PD; q++)
-      if (q < nt) { la.issue(kt0 + q, smem + q * S::STAGE); lb.issue(kt0 + q, smem + q * S::STAGE + S::ABYTES); }
+      if (q < nt) {
+        if constexpr (REGA) la.issue_regs(kt0 + q, areg); else la.issue(kt0 + q, smem + q * S::STAGE);
+        lb.issue(kt0 + q, smem + q * S::STAGE + S::ABYTES);
+      }
     if constexpr (PD == 2) { if (nt > 1) wait_vmcnt<NL>(); else wait_vmcnt<0>(); }
     else wait_vmcnt<0>();
+    if constexpr (REGA) { la.commit(smem, areg, kt0); wait_lgkm0(); }
     __builtin_amdgcn_s_barrier();
     read_frags(0, smem, 0);
     int cur = 0;
@@ -742,7 +808,7 @@ __global__ void __launch_bounds__(GEMM_THREADS) igemm_kernel(LA la, LB lb, EPI e
       if (pre) {
         int st = cur + PD; if (st >= NST) st -= NST;
         char* nx = smem + st * S::STAGE;
-        la.issue(kt0 + t + PD, nx);
+        if constexpr (REGA) la.issue_regs(kt0 + t + PD, areg); else la.issue(kt0 + t + PD, nx);
         lb.issue(kt0 + t + PD, nx + S::ABYTES);
       }
       const char* stg = smem + cur * S::STAGE;
@@ -756,6 +822,7 @@ __global__ void __launch_bounds__(GEMM_THREADS) igemm_kernel(LA la, LB lb, EPI e
           // tile t+1 landed (own DMAs): PD-1 newer tiles may stay in flight
           if constexpr (PD == 2) { if (pre) wait_vmcnt<NL>(); else wait_vmcnt<0>(); }
           else wait_vmcnt<0>();
+          if constexpr (REGA) la.commit(smem + nxt * S::STAGE, areg, kt0 + t + 1);   // stage nxt: read last in t-1
           wait_lgkm0();
           __builtin_amdgcn_s_barrier();
           read_frags(b ^ 1, smem + nxt * S::STAGE, 0);

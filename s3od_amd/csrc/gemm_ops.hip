@@ -1008,6 +1008,23 @@ static int conv_fwd_igemm(int dtype, ConvGeo g, int M, int N, int K, int Cin, in
   return 0;
 }
 
+// LayerNorm fused into the QKV+RoPE projection's A operand (bf16; measurement prototype for north_star's
+// "fused LayerNorm+QKV projection", not used by the engine): x: [B*Ntok][D] fp32 residual stream, mean / rstd:
+// [B*Ntok] (s3od_layernorm_fwd with y = nullptr), ln_w / ln_b: [D]; outputs as s3od_qkv_rope_fwd.  128x128 tiles
+// (the register-staged A cannot use the ping-pong kernel's LDS-DMA schedule).
+int s3od_ln_qkv_rope_fwd(int dtype, int B, int Ntok, int P, int H, const float* x, const float* mean, const float* rstd,
+                         const float* ln_w, const float* ln_b, const void* w, const float* bias, const float* cos_t,
+                         const float* sin_t, void* q, void* k, void* v, void* stream) {
+  S3OD_REQUIRE(dtype == S3OD_BF16, "ln_qkv_rope_fwd: bf16 only");
+  const int D = 64 * H, N = 3 * D, M = B * Ntok;
+  LnA<128> la{x, (long)D, M, D, mean, rstd, ln_w, ln_b};
+  DenseKC<bf16, 128> lb{(const bf16*)w, (long)D, N, D, 0};
+  EpiQKV<bf16> e{(bf16*)q, (bf16*)k, (bf16*)v, bias, cos_t, sin_t, M, Ntok, P, H};
+  S3OD_REQUIRE(la.buf_ok(), "ln_qkv_rope_fwd: operand window too large");
+  return launch_igemm<bf16, 128, 128, decltype(la), decltype(lb), decltype(e), 2>(la, lb, e, M, N, cdiv(D, 64), 1, 1,
+                                                                                   (hipStream_t)stream);
+}
+
 // ---------------------------------------------------------------------------------- convs
 // NHWC activations, weights repacked [Cout][KH][KW][Cin].
 // pre = conv(relu?(x)) + bias[n]; out[b,oy,ox,n] = act(pre*scale[n] + shift[n]) (+res1 +res2);

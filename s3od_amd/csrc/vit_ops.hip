@@ -87,6 +87,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
   for (int i = 0; i < 4 * NV; i++) { float d = v[i] - mean; q += d * d; }
   float var = warp_sum(q) * (1.0f / D);
   float rstd = 1.0f / sqrtf(var + eps);
+  if (y) {                                         // y == nullptr: statistics only
   T* yr = y + (long)row * D;
 #pragma unroll
   for (int i = 0; i < NV; i++) {
@@ -96,6 +97,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
     float o2 = (v[4 * i + 2] - mean) * rstd * wf.z + bf.z, o3 = (v[4 * i + 3] - mean) * rstd * wf.w + bf.w;
     if constexpr (sizeof(T) == 4) *(float4*)(yr + c) = make_float4(o0, o1, o2, o3);
     else { bf16x4 o = {(bf16)o0, (bf16)o1, (bf16)o2, (bf16)o3}; *(bf16x4*)(yr + c) = o; }
+  }
   }
   if (lane == 0) { mean_o[row] = mean; rstd_o[row] = rstd; }
 }
