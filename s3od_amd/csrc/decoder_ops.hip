@@ -28,7 +28,8 @@ __global__ void repack_kernel(const float* __restrict__ src, T* __restrict__ dst
 // {src ptr, dst ptr, O, I, KH*KW, dst element offset, mode, dst leading dim}; chunk_t / chunk_o map
 // blocks -> (tensor, start).  mode 0: dst [O][KHW][I] (the conv / linear kernel layout);
 // mode 1: dst [I][KHW][ld] with column o (+offset) and the taps reversed — the stride-1 conv's
-// data-gradient weight (dx = conv(dy, w^T flipped)), several tensors may interleave their columns.
+// data-gradient weight (dx = conv(dy, w^T flipped)), several tensors may interleave their columns;
+// mode 2: as mode 1 without the tap reversal (the ConvTranspose2d(4, s2) sub-pixel kernel's weight).
 constexpr int RPK_FIELDS = 8;
 template <typename T>
 __global__ void __launch_bounds__(256) repack_multi_kernel(const long* __restrict__ tab, const int* __restrict__ chunk_t,
@@ -48,7 +49,7 @@ __global__ void __launch_bounds__(256) repack_multi_kernel(const long* __restric
       dst[idx] = from_f<T>(src[((long)o * I + i) * KHW + tp]);
     } else {
       int o = idx % O; long r = idx / O; int tp = r % KHW; int i = r / KHW;
-      dst[((long)i * KHW + tp) * ld + o] = from_f<T>(src[((long)o * I + i) * KHW + (KHW - 1 - tp)]);
+      dst[((long)i * KHW + tp) * ld + o] = from_f<T>(src[((long)o * I + i) * KHW + (mode == 1 ? KHW - 1 - tp : tp)]);
     }
   }
 }

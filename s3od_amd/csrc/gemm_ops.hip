@@ -317,7 +317,7 @@ static int launch_halo(const bf16* x, const bf16* w, EPI epi, int B, int H, int 
   if (tiles * HT_TH * HT_TW >= (1L << 31)) { s3od_set_error("halo conv: too many pixels"); return 22; }
   static int ncu = 0;
   if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
-  const int nwg = (int)std::min<long>(tiles, (long)ncu);       // one persistent workgroup per CU
+  const int nwg = (int)std::min<long>(std::max<long>(tiles, 8), (long)ncu);   // one persistent WG per CU, >= 8 so every XCD owns its range
   hipLaunchKernelGGL(kfn, dim3(nwg), dim3(512), S::LDS, st, x, w, epi, H, W, tx, ty, (int)tiles);
   return s3od_check_launch("conv3x3_halo");
 }
@@ -626,10 +626,170 @@ static int launch_rw(const bf16* x, const bf16* w, const float* bias, const bf16
   if (tiles >= (1L << 31)) { s3od_set_error("conv rw: too many tiles"); return 22; }
   static int ncu = 0;
   if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
-  const int nwg = (int)std::min<long>(tiles, (long)ncu);       // one persistent workgroup per CU
+  const int nwg = (int)std::min<long>(std::max<long>(tiles, 8), (long)ncu);   // one persistent WG per CU, >= 8 so every XCD owns its range
   hipLaunchKernelGGL(kfn, dim3(nwg), dim3(256), S::LDS, st, x, w, bias, res1, colsum, out, H, W, tx, ty, (int)tiles, w2, b2,
                      logits);
   return s3od_check_launch("conv3x3_c64_rw");
+}
+
+// ---------------------------------------------------------------- register-weight ConvTranspose2d(128, 64, 4, s2, p1)
+// upsample_2x.0 of the output head (src/s3od/model.py:146-153: 512^2 x 128 -> 1024^2 x 64, bias, ReLU) moves 3.2 GB
+// per call at bs 16; the generic path (conv data gradient, one implicit GEMM per output parity class) ran it at
+// 2.56 ms.  Sub-pixel decomposition: output pixel (2j + py, 2i + px) = bias + sum over the 2 x 2 taps
+// ky = 1 - py + 2a, kx = 1 - px + 2c of x[j + py - a][i + px - c] . W[:, :, ky, kx], i.e. four 2x2 convs of x.
+//   * tile = 8 x 16 input pixels (-> 16 x 32 output pixels); its (8+2) x (16+2) x 128 halo arrives by LDS-DMA into a
+//     3-deep ring, rows padded to 288 B (two dummy 16-B slots, conflict-free ds_read_b128 for every tap offset);
+//   * wave w: output row parity py = w >> 1, output channels 32 (w & 1) .. +31, both column parities in turn; its
+//     2 classes x 4 taps x 128 x 32 weights sit in registers as MFMA A fragments (256 VGPRs, gathered once);
+//   * epilogue as in the 3x3 kernel: bias is the accumulators' initial value, ReLU, lane-pair channel trade,
+//     one 16-B store per lane per 16-pixel block (stride-2 output columns; the other parity's wave fills the gaps).
+namespace ct {
+constexpr int TH = 8, TW = 16, HC = TW + 2, PX = (TH + 2) * HC, ROWB = 288;          // 18 slots of 16 B per pixel
+constexpr int PIECES = ((PX * ROWB + 4095) / 4096) * 4, PPW = PIECES / 4, BUF = PIECES * 1024, LDS = 3 * BUF + 1024;
+static_assert(LDS <= 160 * 1024, "convT LDS budget");
+}  // namespace ct
+template <bool RELU>
+__global__ void __launch_bounds__(256, 1) convT4s2_rw_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wt,
+                                                              const float* __restrict__ bias, bf16* __restrict__ out,
+                                                              int H, int W, int tiles_x, int tiles_y, int ntiles) {
+  using namespace ct;
+  constexpr int NS = 16;                                            // stores per tile per wave (2 classes x 8 rows)
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int lr = lane & 15, lg = lane >> 4, odd = lg & 1;
+  const int py = wave >> 1, ch0 = 32 * (wave & 1);
+  const int nwg = gridDim.x, xcd = blockIdx.x & 7, wpx = (nwg + 7 - xcd) >> 3, wi = blockIdx.x >> 3;
+  const int t_beg = (int)((long)ntiles * xcd / 8), t_end = (int)((long)ntiles * (xcd + 1) / 8);
+  const long img_i = (long)H * W * 128, img_o = (long)4 * H * W * 64;
+
+  // weights: wt = [co = 64][ky][kx][ci = 128] (ConvTranspose2d weight [128][64][4][4] transposed, s3od_repack_multi
+  // mode 2); wr[pxc][s][nb], s = (2a + c) * 4 + kk: lane (lr, lg) holds W[co = ch0 + 16 nb + lr][ky][kx][ci = 32 kk + 8 lg ..]
+  bf16x8 wr[2][16][2];
+#pragma unroll
+  for (int pxc = 0; pxc < 2; pxc++)
+#pragma unroll
+    for (int s = 0; s < 16; s++)
+#pragma unroll
+      for (int nb = 0; nb < 2; nb++) {
+        const int a = s >> 3, c = (s >> 2) & 1, kk = s & 3, ky = 1 - py + 2 * a, kx = 1 - pxc + 2 * c;
+        wr[pxc][s][nb] = *(const bf16x8*)(wt + ((ch0 + nb * 16 + lr) * 16 + ky * 4 + kx) * 128 + kk * 32 + lg * 8);
+      }
+  int dm[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; i++) {
+    const int b = (wave * PPW + i) * 1024 + lane * 16, px = b / ROWB, ch = (b % ROWB) >> 4;
+    dm[i] = (px < PX && ch < 16) ? ((px / HC) << 16) | ((px % HC) << 4) | ch : -1;
+  }
+  auto issue = [&](int tile, int slot) {
+    const bool live = tile < t_end;
+    const int tc = live ? tile : t_beg;
+    const int txi = tc % tiles_x, t2 = tc / tiles_x, tyi = t2 % tiles_y, bb = t2 / tiles_y;
+    const int ty0 = tyi * TH - 1, tx0 = txi * TW - 1;
+    const auto r = make_rsrc(x + bb * img_i, (unsigned long)img_i * 2);
+    char* dst = smem + slot * BUF + wave * PPW * 1024;
+#pragma unroll
+    for (int i = 0; i < PPW; i++) {
+      const int v = dm[i], gy = ty0 + (v >> 16), gx = tx0 + ((v >> 4) & 0xfff);
+      const bool ok = live && v >= 0 && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+      blds16(r, ok ? (unsigned)((gy * W + gx) * 256 + (v & 15) * 16) : 0x80000000u, dst + i * 1024);
+    }
+  };
+  // halo pixel of (row r, tap a, column parity pxc, tap c) for lane lr: (r + 1 + py - a) * HC + lr + 1 + pxc - c
+  const int lbase = (lr + HC * py) * ROWB + lg * 16;
+  const int cb = ch0 + (odd ? 16 : 0) + 8 * (lg >> 1);
+  float* aux = (float*)(smem + 3 * BUF);
+  if (tid < 64) aux[tid] = bias ? bias[tid] : 0.f;
+  __syncthreads();
+
+  int tile = t_beg + wi, k = 0;
+  issue(tile, 0);
+  issue(tile + wpx, 1);
+  for (; tile < t_end; tile += wpx, k++) {
+    const int txi = tile % tiles_x, t2 = tile / tiles_x, tyi = t2 % tiles_y, bb = t2 / tiles_y;
+    const auto ro = make_rsrc(out + bb * img_o, (unsigned long)img_o * 2);
+    if (k == 0) wait_vmcnt<PPW>();
+    else if (k == 1) wait_vmcnt<PPW + NS>();
+    else wait_vmcnt<NS + PPW + NS>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(tile + 2 * wpx, (k + 2) % 3);
+    const char* hb = smem + (k % 3) * BUF + lbase;
+#pragma unroll
+    for (int pxc = 0; pxc < 2; pxc++) {
+      f32x4 acc[8][2];
+#pragma unroll
+      for (int nb = 0; nb < 2; nb++) {
+        const f32x4 b0 = *(const f32x4*)(aux + ch0 + nb * 16 + 4 * lg);
+#pragma unroll
+        for (int r = 0; r < 8; r++) acc[r][nb] = b0;
+      }
+      auto rd = [&](int s, bf16x8 (&fa)[8]) {
+        const int a = s >> 3, c = (s >> 2) & 1, kk = s & 3;
+#pragma unroll
+        for (int r = 0; r < 8; r++) fa[r] = *(const bf16x8*)(hb + ((r + 1 - a) * HC + 1 + pxc - c) * ROWB + kk * 64);
+      };
+      auto mm = [&](int s, const bf16x8 (&fa)[8]) {
+#pragma unroll
+        for (int r = 0; r < 8; r++)
+#pragma unroll
+          for (int nb = 0; nb < 2; nb++)
+            acc[r][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[pxc][s][nb], fa[r], acc[r][nb], 0, 0, 0);
+      };
+      bf16x8 fa0[8], fa1[8];
+      rd(0, fa0);
+#pragma unroll
+      for (int s = 0; s < 16; s += 2) {
+        rd(s + 1, fa1);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(s, fa0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 2 < 16) rd(s + 2, fa0);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(s + 1, fa1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      const int gx = txi * TW + lr;
+#pragma unroll
+      for (int r = 0; r < 8; r++) {
+        const int gy = tyi * TH + r;
+        const unsigned po = (gy < H && gx < W) ? (unsigned)(((2 * gy + py) * 2 * W + 2 * gx + pxc) * 128 + cb * 2) : 0x80000000u;
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          float v0 = acc[r][0][e], v1 = acc[r][1][e];
+          if (RELU) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); }
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(v0), __float_as_uint(v1), false, false);
+          o[e] = __uint_as_float(sw[0]);
+          o[4 + e] = __uint_as_float(sw[1]);
+        }
+        bf16x8 ob;
+#pragma unroll
+        for (int e = 0; e < 8; e++) ob[e] = (bf16)o[e];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, ob), ro, po, 0, 0);
+      }
+    }
+  }
+  wait_vmcnt<0>();
+}
+
+// S3OD_CONVT_RW=0 disables the path (read per call)
+static bool convt_rw_ok(int dtype, int B, int H, int W) {
+  const char* e = getenv("S3OD_CONVT_RW");
+  return dtype == S3OD_BF16 && !(e && atoi(e) == 0) && B > 0 && (long)4 * H * W * 128 < (1L << 31);
+}
+static int launch_convt_rw(const bf16* x, const bf16* wt, const float* bias, bool relu, bf16* out, int B, int H, int W,
+                           hipStream_t st) {
+  auto kfn = relu ? convT4s2_rw_kernel<true> : convT4s2_rw_kernel<false>;
+  static bool attr[2] = {false, false};
+  if (!attr[relu]) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, ct::LDS); attr[relu] = true; }
+  const int tx = cdiv(W, ct::TW), ty = cdiv(H, ct::TH);
+  const long tiles = (long)B * tx * ty;
+  if (tiles >= (1L << 31)) { s3od_set_error("convT rw: too many tiles"); return 22; }
+  static int ncu = 0;
+  if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
+  const int nwg = (int)std::min<long>(std::max<long>(tiles, 8), (long)ncu);   // >= 8: every XCD owns a tile range
+  hipLaunchKernelGGL(kfn, dim3(nwg), dim3(256), ct::LDS, st, x, wt, bias, out, H, W, tx, ty, (int)tiles);
+  return s3od_check_launch("convT4s2_rw");
 }
 
 // ---------------------------------------------------------------- halo ping-pong 3x3 conv launcher
@@ -796,6 +956,119 @@ static int launch_wgrad_halo(const bf16* dy, const bf16* x, float* ws, int B, in
   const int wpc = (int)std::max<long>(1, std::min<long>(tiles, std::max(1, ncu / nblk)));
   hipLaunchKernelGGL(kfn, dim3(nblk * wpc), dim3(S::NT), S::LDS, st, dy, x, ws, H, W, tx, ty, (int)tiles, CinT, CoT, nci, wpc);
   return s3od_check_launch("conv3x3_wgrad_halo");
+}
+
+// LDS-DMA form of the 64-channel-block halo wgrad (Cout block 64): the dy tile (256 px x 64) and the x halo
+// (10 x 34 px x 64) of the NEXT tile land by buffer_load ... lds into the other half of a 2-deep ring while this
+// tile's MFMAs run, so there is no register staging (PT x 4 VGPRs), no ds_write and one barrier per tile.  The
+// DMA lanes pick the global 16-B chunk that the XOR swizzle (dy_at / hx_at) puts at their LDS position.
+namespace wgd {
+constexpr int DYB = 256 * 128, HXB = HT_PX * 128, PIECES = 76, PPW = PIECES / 4, BUF = PIECES * 1024, LDS = 2 * BUF;
+static_assert(DYB % 1024 == 0 && DYB + HXB <= BUF && LDS <= 160 * 1024, "wgrad dma layout");
+}  // namespace wgd
+template <bool RELU>
+__global__ void __launch_bounds__(256, 1)
+conv3x3_wgrad_dma_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, float* __restrict__ ws, int H, int W,
+                         int tiles_x, int tiles_y, int ntiles, int CinT, int CoT, int nci, int wpc) {
+  using namespace wgd;
+  constexpr int NCO = 4, NP = 9;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  // channel block of this workgroup and its contiguous tile range (as in the register-staged kernel; an XCD-grouped
+  // order that runs the channel blocks of one tile behind one L2 measured the same)
+  const int combo = blockIdx.x / wpc, wi = blockIdx.x - combo * wpc;
+  const int t_beg = (int)((long)ntiles * wi / wpc), t_end = (int)((long)ntiles * (wi + 1) / wpc);
+  const int co0 = (combo / nci) * 64, ci0 = (combo % nci) * 64;
+  const int pair0 = NP * wave;
+  f32x4 acc[NP][NCO];
+#pragma unroll
+  for (int i = 0; i < NP; i++)
+#pragma unroll
+    for (int j = 0; j < NCO; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // piece p = PPW wave + i: bytes [1024 p, +1024) of a ring slot; pieces < 32 = dy image [256 px][128 B],
+  // the rest = halo image [340 px][128 B] (beyond it: dummy).  dm = (row y << 16) | (col x << 4) | logical chunk
+  int dm[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; i++) {
+    const int p = wave * PPW + i, b = p * 1024 + lane * 16;
+    if (p < DYB / 1024) {
+      const int row = b >> 7, c = ((b >> 4) & 7) ^ (row & 7);
+      dm[i] = ((row / HT_TW) << 16) | ((row % HT_TW) << 4) | c;
+    } else {
+      const int hb = b - DYB, row = hb >> 7, c = ((hb >> 4) & 7) ^ (row & 7);
+      dm[i] = row < HT_PX ? ((row / HT_HC) << 16) | ((row % HT_HC) << 4) | c : -1;
+    }
+  }
+  auto issue = [&](int tile, int slot) {
+    const int txi = tile % tiles_x, t2 = tile / tiles_x, tyi = t2 % tiles_y, b = t2 / tiles_y;
+    const int ty0 = tyi * HT_TH, tx0 = txi * HT_TW;
+    const long img_d = (long)H * W * CoT, img_x = (long)H * W * CinT;
+    const auto rd = make_rsrc(dy + b * img_d, (unsigned long)img_d * 2);
+    const auto rx = make_rsrc(x + b * img_x, (unsigned long)img_x * 2);
+    char* dst = smem + slot * BUF + wave * PPW * 1024;
+#pragma unroll
+    for (int i = 0; i < PPW; i++) {
+      const int p = wave * PPW + i, v = dm[i];
+      if (p < DYB / 1024) {                              // wave-uniform
+        const int gy = ty0 + (v >> 16), gx = tx0 + ((v >> 4) & 0xfff);
+        const bool ok = gy < H && gx < W;
+        blds16(rd, ok ? (unsigned)(((gy * W + gx) * CoT + co0) * 2 + (v & 15) * 16) : 0x80000000u, dst + i * 1024);
+      } else {
+        const int gy = ty0 - 1 + (v >> 16), gx = tx0 - 1 + ((v >> 4) & 0xfff);
+        const bool ok = v >= 0 && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+        blds16(rx, ok ? (unsigned)(((gy * W + gx) * CinT + ci0) * 2 + (v & 15) * 16) : 0x80000000u, dst + i * 1024);
+      }
+    }
+  };
+  int tile = t_beg, k = 0;
+  if (tile < t_end) issue(tile, 0);
+  for (; tile < t_end; tile++, k++) {
+    wait_vmcnt<0>();                                     // this tile's pieces (the only vector-memory ops in flight)
+    __builtin_amdgcn_s_barrier();                        // ... of every wave; every wave done with the other slot
+    asm volatile("" ::: "memory");
+    if (tile + 1 < t_end) issue(tile + 1, (k + 1) & 1);
+    const char* dyi = smem + (k & 1) * BUF;
+    const char* hxi = dyi + DYB;
+    for (int ty = 0; ty < HT_TH; ty++) {                  // K step = one output row of 32 pixels
+      bf16x8 fa[NCO];
+#pragma unroll
+      for (int cb = 0; cb < NCO; cb++) fa[cb] = trf(dyi, ty * HT_TW, cb * 16, lane, dy_at<64>);
+#pragma unroll
+      for (int j = 0; j < NP; j++) {
+        const int pr = pair0 + j, tap = pr >> 2, cib = pr & 3, tdy = tap / 3, tdx = tap - tdy * 3;
+        bf16x8 fb = trf(hxi, (ty + tdy) * HT_HC + tdx, cib * 16, lane, hx_at);
+        if constexpr (RELU) fb = __builtin_bit_cast(bf16x8, relu16<bf16>(__builtin_bit_cast(uint4, fb)));
+#pragma unroll
+        for (int cb = 0; cb < NCO; cb++) acc[j][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[cb], fb, acc[j][cb], 0, 0, 0);
+      }
+    }
+  }
+  const int g = lane >> 4, li = lane & 15;
+#pragma unroll
+  for (int j = 0; j < NP; j++) {
+    const int pr = pair0 + j, tap = pr >> 2, cib = pr & 3;
+#pragma unroll
+    for (int cb = 0; cb < NCO; cb++)
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        atomicAdd(ws + (long)(co0 + cb * 16 + 4 * g + r) * (9 * CinT) + tap * CinT + ci0 + cib * 16 + li, acc[j][cb][r]);
+  }
+}
+
+// S3OD_WGRAD_DMA=0 (read per call) keeps the register-staged kernel
+template <bool RELU>
+static int launch_wgrad_dma(const bf16* dy, const bf16* x, float* ws, int B, int H, int W, int CinT, int CoT, hipStream_t st) {
+  auto kfn = conv3x3_wgrad_dma_kernel<RELU>;
+  static bool attr = false;
+  if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, wgd::LDS); attr = true; }
+  const int tx = cdiv(W, HT_TW), ty = cdiv(H, HT_TH);
+  const long tiles = (long)B * tx * ty;
+  static int ncu = 0;
+  if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
+  const int nci = CinT / 64, nblk = (CoT / 64) * nci;
+  const int wpc = (int)std::max<long>(1, std::min<long>(tiles, std::max(1, ncu / nblk)));
+  hipLaunchKernelGGL(kfn, dim3(nblk * wpc), dim3(256), wgd::LDS, st, dy, x, ws, H, W, tx, ty, (int)tiles, CinT, CoT, nci, wpc);
+  return s3od_check_launch("conv3x3_wgrad_dma");
 }
 
 template <int BM, int BN> struct Tile {};
@@ -1060,12 +1333,18 @@ int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int C
 }
 
 // conv dgrad == ConvTranspose2d forward.  dy: [B,OH,OW,Cout] (conv output grid); w: [Cout][KH][KW][Cin];
-// dx: [B,H,W,Cin] (conv input grid).  One launch per output parity class.
+// dx: [B,H,W,Cin] (conv input grid).  One launch per output parity class.  wT (nullable, bf16): [Cin][KH][KW][Cout],
+// taps reversed for 3x3 s1 (the data gradient as a forward conv of dy), as-is for the 4x4 s2 sub-pixel kernel.
 int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW,
                     int stride, int pad, const void* dy, const void* wp,
                     const float* bias, const float* scale, const float* shift, int act, const void* res1,
                     const void* res2, void* dx, void* pre, double* stats, float* colsum, const void* wT, void* stream) {
   S3OD_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "conv_dgrad: channels %% 8");
+  if (wT && KH == 4 && KW == 4 && stride == 2 && pad == 1 && H == 2 * OH && W == 2 * OW && Cout == 128 && Cin == 64 && !scale &&
+      !shift && !res1 && !res2 && !pre && !stats && !colsum && (act == ACT_NONE || act == ACT_RELU) && convt_rw_ok(dtype, B, OH, OW))
+    // ConvTranspose2d(128, 64, 4, 2, 1) forward (upsample_2x.0): the register-weight sub-pixel kernel; wT =
+    // [Cin = 64][4][4][Cout = 128], the conv-view weight transposed WITHOUT tap reversal (s3od_repack_multi mode 2)
+    return launch_convt_rw((const bf16*)dy, (const bf16*)wT, bias, act == ACT_RELU, (bf16*)dx, B, OH, OW, (hipStream_t)stream);
   if (wT && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && Cin == 64 && (Cout == 64 || Cout == 96) &&
       !bias && !scale && !shift && !res2 && !pre && !stats && act == ACT_RELU_BWD && res1 && rw_ok(dtype, B, H, W))
     // stride-1 3x3 data gradient = forward conv of dy with the transposed, tap-reversed weight wT ([Cin][3][3][Cout])
@@ -1139,7 +1418,10 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
   const int coblk = Cout % 64 == 0 ? 64 : (Cout == 96 ? 96 : 0);
   if (wg_knob && dtype == S3OD_BF16 && ws && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W &&
       Cin % 64 == 0 && coblk && (Cin == 64 || (long)H * W >= 512L * 512)) {
-    int rc = coblk == 64 ? (relu_x ? launch_wgrad_halo<64, true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)
+    const bool dma = coblk == 64 && (long)H * W * (Cin > Cout ? Cin : Cout) * 2 < (1L << 31) && !getenv_zero("S3OD_WGRAD_DMA");
+    int rc = dma ? (relu_x ? launch_wgrad_dma<true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)
+                           : launch_wgrad_dma<false>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)) :
+             coblk == 64 ? (relu_x ? launch_wgrad_halo<64, true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)
                                    : launch_wgrad_halo<64, false>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st))
                          : (relu_x ? launch_wgrad_halo<96, true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)
                                    : launch_wgrad_halo<96, false>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st));

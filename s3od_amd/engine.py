@@ -112,10 +112,11 @@ class DPTEngine:
             ents[self.dt].append((P[name], dst, off, O, I, KH * KW, 0, 0))
             return dst
 
-        def pack_dgrad(name, O, I, dst, off, ld):
+        def pack_dgrad(name, O, I, dst, off, ld, KHW=9, mode=1):
             """[I][3][3][ld] transposed + tap-reversed copy (column off..off+O): the weight of the
-            stride-1 3x3 conv's data gradient run as a forward conv (s3od_conv_dgrad's wT)."""
-            ents[self.dt].append((P[name], dst, off, O, I, 9, 1, ld))
+            stride-1 3x3 conv's data gradient run as a forward conv (s3od_conv_dgrad's wT); mode 2: transposed
+            without the tap reversal."""
+            ents[self.dt].append((P[name], dst, off, O, I, KHW, mode, ld))
 
         def copy32(name, dst, off, n):
             ents[F32].append((P[name], dst, off, n, 1, 1, 0, 0))
@@ -170,6 +171,8 @@ class DPTEngine:
                 pack_dgrad(h + f"scratch.layer{i + 1}_rn.weight", 256, c, w[f"rn{i + 1}T"], 0, 256)
             w["oc1T"] = torch.empty((256, 3, 3, 128), dtype=T, device=dev)
             pack_dgrad(m + "output_conv1.weight", 128, 256, w["oc1T"], 0, 128)
+            w["up2xT"] = torch.empty((64, 4, 4, 128), dtype=T, device=dev)       # ConvT sub-pixel kernel weight
+            pack_dgrad(m + "upsample_2x.0.weight", 128, 64, w["up2xT"], 0, 128, KHW=16, mode=2)
             w["c64T"] = torch.empty((64, 3, 3, 64), dtype=T, device=dev)
             pack_dgrad(m + "upsample_2x.2.weight", 64, 64, w["c64T"], 0, 64)
             w["heads1T"] = torch.empty((64, 3, 3, 32 * nm), dtype=T, device=dev)
@@ -208,13 +211,14 @@ class DPTEngine:
               bias, scale, shift, act, res1, res2, out, pre, stats, colsum, stream())
         return out
 
-    def _convT(self, x, w, B, IH, IW, Cin_T, Cout_T, k, s, p, bias=None, act=ACT_NONE, out=None):
-        """ConvTranspose2d forward == conv dgrad with the conv-view weight (no flip)."""
+    def _convT(self, x, w, B, IH, IW, Cin_T, Cout_T, k, s, p, bias=None, act=ACT_NONE, out=None, wT=None):
+        """ConvTranspose2d forward == conv dgrad with the conv-view weight (no flip); wT: the transposed copy
+        [Cout_T][k][k][Cin_T] for the 4x4 s2 sub-pixel kernel (bf16)."""
         OH, OW = (IH - 1) * s - 2 * p + k, (IW - 1) * s - 2 * p + k
         if out is None:
             out = torch.empty((B, OH, OW, Cout_T), dtype=self.tdt, device=x.device)
         lib()("s3od_conv_dgrad", self.dt, B, OH, OW, Cout_T, IH, IW, Cin_T, k, k, s, p, x, w,
-              bias, None, None, act, None, None, out, None, None, None, None, stream())
+              bias, None, None, act, None, None, out, None, None, None, wT, stream())
         return out
 
     def _bilinear(self, x, B, IH, IW, OH, OW, C):
@@ -390,7 +394,8 @@ class DPTEngine:
         # mask head (src/s3od/model.py:455-467)
         m = h + "mask_head."
         oc1 = self._conv(p1, W8["oc1"], B, H1, W1, 256, 128, 3, 1, 1, bias=P[m + "output_conv1.bias"])
-        up = self._convT(oc1, W8["up2x"], B, H1, W1, 128, 64, 4, 2, 1, bias=P[m + "upsample_2x.0.bias"], act=ACT_RELU)
+        up = self._convT(oc1, W8["up2x"], B, H1, W1, 128, 64, 4, 2, 1, bias=P[m + "upsample_2x.0.bias"], act=ACT_RELU,
+                         wT=W8.get("up2xT"))
         HH, WW = up.shape[1], up.shape[2]
         c64 = self._conv(up, W8["c64"], B, HH, WW, 64, 64, 3, 1, 1, bias=P[m + "upsample_2x.2.bias"], act=ACT_RELU)
         # F.interpolate(size=(16ph,16pw), antialias=True) is an exact identity here (HH == 16*ph)

@@ -147,3 +147,35 @@ def test_conv_dgrad_via_transposed_weight(cin, cout, H, W):
     ref_cs = ref.sum((0, 2, 3))
     tol = 2e-3 * ref.abs().sum((0, 2, 3)).max()
     assert float((cs - ref_cs).abs().max()) <= float(tol), (float((cs - ref_cs).abs().max()), float(tol))
+
+
+@pytest.mark.parametrize("B,H,W,relu", [(2, 19, 37, True), (1, 32, 48, False), (3, 8, 16, True), (1, 70, 9, True)])
+def test_convT_4s2_register_weight(B, H, W, relu):
+    """upsample_2x.0 = ConvTranspose2d(128, 64, 4, stride 2, pad 1) + bias (+ ReLU) on the register-weight sub-pixel
+    kernel (csrc/gemm_ops.hip convT4s2_rw_kernel; reference module src/s3od/model.py:146-153) vs fp32
+    conv_transpose2d of the same bf16 operands; ragged input maps exercise partial 8 x 16 tiles.  The generic
+    per-parity-class implicit GEMM (S3OD_CONVT_RW=0, read per call) is checked against the same reference."""
+    import os
+    from s3od_amd._lib import lib, stream
+    g = torch.Generator(device="cuda").manual_seed(B * H * W)
+    x = torch.randn(B, 128, H, W, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(128, 64, 4, 4, device="cuda", generator=g) * 0.03).bfloat16()      # ConvT [Cin][Cout][4][4]
+    bias = torch.randn(64, device="cuda", generator=g) * 0.1
+    ref = F.conv_transpose2d(x.float(), w.float(), bias, stride=2, padding=1)
+    if relu:
+        ref = F.relu(ref)
+    wp = w.permute(0, 2, 3, 1).contiguous()                                              # conv view [128][4][4][64]
+    wT = w.permute(1, 2, 3, 0).contiguous()                                              # [64][4][4][128] (no flip)
+    outs = []
+    for knob in ("1", "0"):
+        os.environ["S3OD_CONVT_RW"] = knob
+        try:
+            out = torch.full((B, 2 * H, 2 * W, 64), float("nan"), device="cuda", dtype=torch.bfloat16)
+            lib()("s3od_conv_dgrad", BF16, B, 2 * H, 2 * W, 64, H, W, 128, 4, 4, 2, 1, _nhwc(x), wp, bias, None, None,
+                  ACT_RELU if relu else 0, None, None, out, None, None, None, wT, stream())
+            torch.cuda.synchronize()
+        finally:
+            os.environ.pop("S3OD_CONVT_RW", None)
+        assert not torch.isnan(out.float()).any(), "every output pixel must be written"
+        _close(out, _nhwc(ref))
+        outs.append(out)

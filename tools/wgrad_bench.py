@@ -1,0 +1,57 @@
+"""A/B of the halo-tile 3x3 weight gradients at bs 16: the LDS-DMA kernel (default) vs the register-staged one
+(S3OD_WGRAD_DMA=0, read per call), one process, interleaved rounds; results compared (dev tool).
+Shapes: upsample_2x.2 (1024^2, 64 -> 64) and output_conv1 (512^2, 256 -> 128, ReLU'd input).
+
+    python tools/wgrad_bench.py
+"""
+import os
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+from s3od_amd._lib import lib, stream, BF16  # noqa: E402
+
+
+def timeit(fn, n=5):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n * 1e-3
+
+
+def main():
+    B = 16
+    for (H, cin, cout, relu) in ((1024, 64, 64, 0), (512, 256, 128, 0), (512, 256, 128, 1)):
+        g = torch.Generator(device="cuda").manual_seed(H + cin)
+        dy = torch.randn(B, H, H, cout, device="cuda", generator=g).bfloat16()
+        x = torch.randn(B, H, H, cin, device="cuda", generator=g).bfloat16()
+        ws = torch.zeros(cout * 9 * cin, device="cuda")
+        fl = 2.0 * B * H * H * cin * cout * 9
+        res = {}
+        for rnd in range(3):
+            for knob in ("0", "1"):
+                os.environ["S3OD_WGRAD_DMA"] = knob
+                dw = torch.zeros(cout, cin, 3, 3, device="cuda")
+                f = lambda: lib()("s3od_conv_wgrad", BF16, B, H, H, cin, H, H, cout, 3, 3, 1, 1, dy, x, relu, dw, ws, 0, stream())
+                t = timeit(f)
+                dw.zero_()
+                f()
+                torch.cuda.synchronize()
+                res[knob] = dw.clone()
+                print(f"{H}^2 {cin}->{cout} relu {relu} round {rnd} DMA={knob}: {t * 1e6:8.1f} us {fl / t / 1e12:7.1f} TF/s", flush=True)
+        b = res["0"]
+        for k in ("1",):
+            a = res[k]
+            print(f"{H}^2 {k}: max |dma - staged| / max|staged| = {float((a - b).abs().max() / b.abs().max()):.3e}")
+    os.environ.pop("S3OD_WGRAD_DMA", None)
+
+
+if __name__ == "__main__":
+    main()
