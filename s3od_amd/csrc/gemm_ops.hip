@@ -772,6 +772,162 @@ __global__ void __launch_bounds__(256, 1) convT4s2_rw_kernel(const bf16* __restr
   wait_vmcnt<0>();
 }
 
+// ---------------------------------------------------------------- register-weight Conv2d(64, 128, 4, s2, p1)
+// The data gradient of upsample_2x.0 (the ConvTranspose2d's input gradient is this strided conv of dy with the
+// same conv-view weight [128][4][4][64]; 1024^2 x 64 -> 512^2 x 128 at bs 16, plus the column sums that are
+// output_conv1's bias gradient).  Same design as the kernels above:
+//   * tile = 4 x 16 output pixels; its (2*4+2) x (2*16+2) x 64 input halo lands by LDS-DMA in a 3-deep ring, pixel
+//     rows padded to 144 B (9 slots, one dummy): the stride-2 tap reads are conflict-free without a swizzle;
+//   * wave w = output channels 32 w .. +31 with their 16 taps x 64 weights in registers (256 VGPRs) as MFMA A
+//     fragments, read straight from the conv-view pack; all waves share the tile's 4 x 16 pixels;
+//   * epilogue: lane-pair channel trade, one 16-B store per lane per 16-pixel row, column sums in fp32 (LDS atomics,
+//     one global add per channel and workgroup).
+static bool convt_rw_ok(int dtype, int B, int H, int W);
+namespace cs2 {
+constexpr int TH = 4, TW = 16, HR = 2 * TH + 2, HC = 2 * TW + 2, PX = HR * HC, ROWB = 144;
+constexpr int PIECES = ((PX * ROWB + 4095) / 4096) * 4, PPW = PIECES / 4, BUF = PIECES * 1024, LDS = 3 * BUF + 1024;
+static_assert(LDS <= 160 * 1024, "conv s2 LDS budget");
+}  // namespace cs2
+__global__ void __launch_bounds__(256, 1) conv4s2_rw_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                             float* __restrict__ colsum, bf16* __restrict__ out, int H,
+                                                             int W, int tiles_x, int tiles_y, int ntiles) {
+  using namespace cs2;
+  constexpr int NS = TH;                                            // stores per tile per wave
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int lr = lane & 15, lg = lane >> 4, odd = lg & 1;
+  const int ch0 = 32 * wave;
+  const int nwg = gridDim.x, xcd = blockIdx.x & 7, wpx = (nwg + 7 - xcd) >> 3, wi = blockIdx.x >> 3;
+  const int t_beg = (int)((long)ntiles * xcd / 8), t_end = (int)((long)ntiles * (xcd + 1) / 8);
+  const int Hi = 2 * H, Wi = 2 * W;
+  const long img_i = (long)Hi * Wi * 64, img_o = (long)H * W * 128;
+  // wr[tap][kk][nb]: lane (lr, lg) holds w[co = ch0 + 16 nb + lr][tap][ci = 32 kk + 8 lg .. +7]
+  bf16x8 wr[16][2][2];
+#pragma unroll
+  for (int tap = 0; tap < 16; tap++)
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+      for (int nb = 0; nb < 2; nb++)
+        wr[tap][kk][nb] = *(const bf16x8*)(w + ((ch0 + nb * 16 + lr) * 16 + tap) * 64 + kk * 32 + lg * 8);
+  int dm[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; i++) {
+    const int b = (wave * PPW + i) * 1024 + lane * 16, px = b / ROWB, ch = (b % ROWB) >> 4;
+    dm[i] = (px < PX && ch < 8) ? ((px / HC) << 16) | ((px % HC) << 4) | ch : -1;
+  }
+  auto issue = [&](int tile, int slot) {
+    const bool live = tile < t_end;
+    const int tc = live ? tile : t_beg;
+    const int txi = tc % tiles_x, t2 = tc / tiles_x, tyi = t2 % tiles_y, bb = t2 / tiles_y;
+    const int iy0 = 2 * tyi * TH - 1, ix0 = 2 * txi * TW - 1;
+    const auto r = make_rsrc(x + bb * img_i, (unsigned long)img_i * 2);
+    char* dst = smem + slot * BUF + wave * PPW * 1024;
+#pragma unroll
+    for (int i = 0; i < PPW; i++) {
+      const int v = dm[i], gy = iy0 + (v >> 16), gx = ix0 + ((v >> 4) & 0xfff);
+      const bool ok = live && v >= 0 && (unsigned)gy < (unsigned)Hi && (unsigned)gx < (unsigned)Wi;
+      blds16(r, ok ? (unsigned)((gy * Wi + gx) * 128 + (v & 15) * 16) : 0x80000000u, dst + i * 1024);
+    }
+  };
+  // halo pixel of output (row r, column lr) and tap (ky, kx): (2 r + ky) * HC + 2 lr + kx
+  const int lbase = 2 * lr * ROWB + lg * 16;
+  const int cb = ch0 + (odd ? 16 : 0) + 8 * (lg >> 1);
+  float* aux = (float*)(smem + 3 * BUF);
+  if (tid < 128) aux[tid] = 0.f;
+  __syncthreads();
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
+  int tile = t_beg + wi, k = 0;
+  issue(tile, 0);
+  issue(tile + wpx, 1);
+  for (; tile < t_end; tile += wpx, k++) {
+    const int txi = tile % tiles_x, t2 = tile / tiles_x, tyi = t2 % tiles_y, bb = t2 / tiles_y;
+    const auto ro = make_rsrc(out + bb * img_o, (unsigned long)img_o * 2);
+    if (k == 0) wait_vmcnt<PPW>();
+    else if (k == 1) wait_vmcnt<PPW + NS>();
+    else wait_vmcnt<NS + PPW + NS>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(tile + 2 * wpx, (k + 2) % 3);
+    const char* hb = smem + (k % 3) * BUF + lbase;
+    f32x4 acc[TH][2];
+#pragma unroll
+    for (int r = 0; r < TH; r++) { acc[r][0] = f32x4{0.f, 0.f, 0.f, 0.f}; acc[r][1] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+    auto rd = [&](int s, bf16x8 (&fa)[TH]) {
+      const int tap = s >> 1, kk = s & 1, ky = tap >> 2, kx = tap & 3;
+#pragma unroll
+      for (int r = 0; r < TH; r++) fa[r] = *(const bf16x8*)(hb + ((2 * r + ky) * HC + kx) * ROWB + kk * 64);
+    };
+    auto mm = [&](int s, const bf16x8 (&fa)[TH]) {
+#pragma unroll
+      for (int r = 0; r < TH; r++)
+#pragma unroll
+        for (int nb = 0; nb < 2; nb++)
+          acc[r][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[s >> 1][s & 1][nb], fa[r], acc[r][nb], 0, 0, 0);
+    };
+    bf16x8 fa0[TH], fa1[TH];
+    rd(0, fa0);
+#pragma unroll
+    for (int s = 0; s < 32; s += 2) {
+      rd(s + 1, fa1);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(s, fa0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 2 < 32) rd(s + 2, fa0);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(s + 1, fa1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int gx = txi * TW + lr;
+#pragma unroll
+    for (int r = 0; r < TH; r++) {
+      const int gy = tyi * TH + r;
+      const bool ok = gy < H && gx < W;
+      const unsigned po = ok ? (unsigned)(((gy * W + gx) * 128 + cb) * 2) : 0x80000000u;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[r][0][e]), __float_as_uint(acc[r][1][e]), false, false);
+        o[e] = __uint_as_float(sw[0]);
+        o[4 + e] = __uint_as_float(sw[1]);
+      }
+      if (ok) {
+#pragma unroll
+        for (int e = 0; e < 8; e++) cs[e] += o[e];
+      }
+      bf16x8 ob;
+#pragma unroll
+      for (int e = 0; e < 8; e++) ob[e] = (bf16)o[e];
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, ob), ro, po, 0, 0);
+    }
+  }
+  if (colsum) {
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      float c = cs[e];
+      c += __shfl_xor(c, 1); c += __shfl_xor(c, 2); c += __shfl_xor(c, 4); c += __shfl_xor(c, 8);
+      if (lr == 0) atomicAdd(aux + cb + e, c);
+    }
+    __syncthreads();
+    if (tid < 128) atomicAdd(colsum + tid, aux[tid]);
+  }
+  wait_vmcnt<0>();
+}
+static int launch_conv4s2_rw(const bf16* x, const bf16* w, float* colsum, bf16* out, int B, int H, int W, hipStream_t st) {
+  auto kfn = conv4s2_rw_kernel;
+  static bool attr = false;
+  if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, cs2::LDS); attr = true; }
+  const int tx = cdiv(W, cs2::TW), ty = cdiv(H, cs2::TH);
+  const long tiles = (long)B * tx * ty;
+  if (tiles >= (1L << 31)) { s3od_set_error("conv s2 rw: too many tiles"); return 22; }
+  static int ncu = 0;
+  if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
+  const int nwg = (int)std::min<long>(std::max<long>(tiles, 8), (long)ncu);
+  hipLaunchKernelGGL(kfn, dim3(nwg), dim3(256), cs2::LDS, st, x, w, colsum, out, H, W, tx, ty, (int)tiles);
+  return s3od_check_launch("conv4s2_rw");
+}
+
 // S3OD_CONVT_RW=0 disables the path (read per call)
 static bool convt_rw_ok(int dtype, int B, int H, int W) {
   const char* e = getenv("S3OD_CONVT_RW");
@@ -1310,6 +1466,10 @@ int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int C
   ConvGeo g{}; g.B = B; g.SH = H; g.SW = W; g.SC = Cin; g.RH = OH; g.RW = OW; g.KH = KH; g.KW = KW; g.s = stride; g.p = pad;
   const int M = B * OH * OW, N = Cout, K = KH * KW * Cin;
   hipStream_t st = (hipStream_t)stream;
+  if (KH == 4 && KW == 4 && stride == 2 && pad == 1 && H == 2 * OH && W == 2 * OW && Cin == 64 && Cout == 128 && !relu_in &&
+      !bias && !scale && !shift && !res1 && !res2 && !pre && !stats && act == ACT_NONE && convt_rw_ok(dtype, B, OH, OW))
+    // the data gradient of upsample_2x.0 (ConvTranspose2d(128, 64, 4, 2, 1)): register-weight strided conv
+    return launch_conv4s2_rw((const bf16*)x, (const bf16*)wp, colsum, (bf16*)out, B, OH, OW, st);
   if (KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && Cin == 64 && Cout == 64 && !relu_in && !stats &&
       !scale && !shift && !res1 && !res2 && !pre && !colsum && (act == ACT_NONE || act == ACT_RELU) && rw_ok(dtype, B, H, W))
     return act == ACT_RELU ? launch_rw<2, 64>((const bf16*)x, (const bf16*)wp, bias, nullptr, nullptr, (bf16*)out, B, H, W, st)

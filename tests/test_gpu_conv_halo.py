@@ -179,3 +179,33 @@ def test_convT_4s2_register_weight(B, H, W, relu):
         assert not torch.isnan(out.float()).any(), "every output pixel must be written"
         _close(out, _nhwc(ref))
         outs.append(out)
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 19, 37), (1, 32, 48), (3, 4, 16), (1, 70, 9)])
+def test_conv_4s2_register_weight_colsum(B, H, W):
+    """The data gradient of upsample_2x.0 = Conv2d(64, 128, 4, stride 2, pad 1) of dy with the conv-view weight
+    [128][4][4][64], plus the column sums (output_conv1's bias gradient), on the register-weight strided kernel
+    (csrc/gemm_ops.hip conv4s2_rw_kernel) and on the implicit GEMM (S3OD_CONVT_RW=0), vs fp32 conv2d of the same
+    bf16 operands (H x W = the output grid; the input is 2H x 2W)."""
+    import os
+    from s3od_amd._lib import lib, stream
+    g = torch.Generator(device="cuda").manual_seed(B + H * W)
+    x = torch.randn(B, 64, 2 * H, 2 * W, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(128, 64, 4, 4, device="cuda", generator=g) * 0.03).bfloat16()
+    ref = F.conv2d(x.float(), w.float(), stride=2, padding=1)                              # [B, 128, H, W]
+    wp = w.permute(0, 2, 3, 1).contiguous()                                              # [128][4][4][64]
+    for knob in ("1", "0"):
+        os.environ["S3OD_CONVT_RW"] = knob
+        try:
+            out = torch.full((B, H, W, 128), float("nan"), device="cuda", dtype=torch.bfloat16)
+            cs = torch.zeros(128, device="cuda")
+            lib()("s3od_conv_fwd", BF16, B, 2 * H, 2 * W, 64, H, W, 128, 4, 4, 2, 1, _nhwc(x), 0, wp, None, None, None, 0,
+                  None, None, out, None, None, cs, stream())
+            torch.cuda.synchronize()
+        finally:
+            os.environ.pop("S3OD_CONVT_RW", None)
+        assert not torch.isnan(out.float()).any(), "every output pixel must be written"
+        _close(out, _nhwc(ref))
+        ref_cs = ref.sum((0, 2, 3))
+        tol = 2e-3 * ref.abs().sum((0, 2, 3)).max()
+        assert float((cs - ref_cs).abs().max()) <= float(tol), (knob, float((cs - ref_cs).abs().max()), float(tol))

@@ -52,6 +52,24 @@ def main():
     for k in ("1",):
         a = outs[k].float()
         print(f"{k}: max |rw - igemm| / max|igemm| = {float((a - b).abs().max() / b.abs().max()):.3e}")
+    # its data gradient: Conv2d(64, 128, 4, s2, p1) of dy (2H x 2W x 64) + column sums
+    dy = torch.randn(B, 2 * H, 2 * H, 64, device="cuda", generator=g).bfloat16()
+    fl2 = 2.0 * B * H * H * 128 * 16 * 64
+    by2 = B * (2 * H) ** 2 * 64 * 2 + B * H * H * 128 * 2
+    res = {}
+    for rnd in range(3):
+        for knob in ("0", "1"):
+            os.environ["S3OD_CONVT_RW"] = knob
+            o = torch.empty(B, H, H, 128, device="cuda", dtype=torch.bfloat16)
+            cs = torch.zeros(128, device="cuda")
+            f = lambda: lib()("s3od_conv_fwd", BF16, B, 2 * H, 2 * H, 64, H, H, 128, 4, 4, 2, 1, dy, 0, wp, None, None, None, 0,
+                              None, None, o, None, None, cs, stream())
+            t = timeit(f)
+            res[knob] = o
+            print(f"dgrad round {rnd} CONVT_RW={knob}: {t * 1e6:8.1f} us  {fl2 / t / 1e12:6.1f} TF/s  {by2 / t / 1e9:6.0f} GB/s", flush=True)
+    os.environ.pop("S3OD_CONVT_RW", None)
+    a, b = res["1"].float(), res["0"].float()
+    print(f"dgrad: max |rw - igemm| / max|igemm| = {float((a - b).abs().max() / b.abs().max()):.3e}")
 
 
 if __name__ == "__main__":
