@@ -1211,6 +1211,119 @@ conv3x3_wgrad_dma_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x
   }
 }
 
+// Weight gradient of the 4x4 / stride-2 / pad-1 conv view of upsample_2x.0 (ConvTranspose2d(128, 64, 4, 2, 1)):
+// dW[co][ky][kx][ci] = sum_p dy[p][co] * x[2p - 1 + (ky, kx)][ci], dy on the OH x OW grid (128 channels), x on the
+// 2OH x 2OW grid (64).  The same LDS-DMA / register-accumulator scheme as the 3x3 kernel above with 16 taps:
+//   * tile = 2 x 32 dy pixels; its x halo (2*2+2) x (2*32+2) is stored column-DE-INTERLEAVED (even / odd halo
+//     columns in two 33-pixel sub-rows), so a tap's 32 stride-2 pixels are 32 consecutive image rows and the
+//     transposed reads keep the swizzle of the 3x3 kernel;
+//   * workgroup = a 64-output-channel block; wave w = taps 4w .. 4w+3 x 4 ci blocks (256 accumulator VGPRs).
+namespace wg4 {
+constexpr int TH = 2, TW = 32, HR = 2 * TH + 2, HS = TW + 1, HPX = HR * 2 * HS;   // halo rows, sub-row length
+constexpr int AB = TH * TW * 128, HB = HPX * 128, PIECES = ((AB + HB + 4095) / 4096) * 4, PPW = PIECES / 4;
+constexpr int BUF = PIECES * 1024, LDS = 2 * BUF;
+static_assert(AB % 1024 == 0 && LDS <= 160 * 1024, "wgrad 4s2 layout");
+}  // namespace wg4
+__global__ void __launch_bounds__(256, 1)
+conv4s2_wgrad_dma_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, float* __restrict__ ws, int OH, int OW,
+                         int tiles_x, int tiles_y, int ntiles, int CinT, int CoT, int nci, int wpc) {
+  using namespace wg4;
+  constexpr int NCO = 4, NP = 16;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int combo = blockIdx.x / wpc, wi = blockIdx.x - combo * wpc;
+  const int t_beg = (int)((long)ntiles * wi / wpc), t_end = (int)((long)ntiles * (wi + 1) / wpc);
+  const int co0 = (combo / nci) * 64, ci0 = (combo % nci) * 64;
+  const int pair0 = NP * wave, IH = 2 * OH, IW = 2 * OW;
+  f32x4 acc[NP][NCO];
+#pragma unroll
+  for (int i = 0; i < NP; i++)
+#pragma unroll
+    for (int j = 0; j < NCO; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // dm = (row << 16) | (column << 4) | logical chunk: dy pieces -> tile row / column; halo -> halo row / halo column
+  int dm[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; i++) {
+    const int p = wave * PPW + i, b = p * 1024 + lane * 16;
+    if (p < AB / 1024) {
+      const int row = b >> 7, c = ((b >> 4) & 7) ^ (row & 7);
+      dm[i] = ((row / TW) << 16) | ((row % TW) << 4) | c;
+    } else {
+      const int hb = b - AB, row = hb >> 7, c = ((hb >> 4) & 7) ^ (row & 7);
+      const int hr = row / (2 * HS), rem = row - hr * 2 * HS, sub = rem / HS, idx = rem - sub * HS;
+      dm[i] = row < HPX ? (hr << 16) | ((2 * idx + sub) << 4) | c : -1;
+    }
+  }
+  auto issue = [&](int tile, int slot) {
+    const int txi = tile % tiles_x, t2 = tile / tiles_x, tyi = t2 % tiles_y, b = t2 / tiles_y;
+    const int oy0 = tyi * TH, ox0 = txi * TW;
+    const long img_d = (long)OH * OW * CoT, img_x = (long)IH * IW * CinT;
+    const auto rd = make_rsrc(dy + b * img_d, (unsigned long)img_d * 2);
+    const auto rx = make_rsrc(x + b * img_x, (unsigned long)img_x * 2);
+    char* dst = smem + slot * BUF + wave * PPW * 1024;
+#pragma unroll
+    for (int i = 0; i < PPW; i++) {
+      const int p = wave * PPW + i, v = dm[i];
+      if (p < AB / 1024) {                               // wave-uniform
+        const int gy = oy0 + (v >> 16), gx = ox0 + ((v >> 4) & 0xfff);
+        const bool ok = gy < OH && gx < OW;
+        blds16(rd, ok ? (unsigned)(((gy * OW + gx) * CoT + co0) * 2 + (v & 15) * 16) : 0x80000000u, dst + i * 1024);
+      } else {
+        const int gy = 2 * oy0 - 1 + (v >> 16), gx = 2 * ox0 - 1 + ((v >> 4) & 0xfff);
+        const bool ok = v >= 0 && (unsigned)gy < (unsigned)IH && (unsigned)gx < (unsigned)IW;
+        blds16(rx, ok ? (unsigned)(((gy * IW + gx) * CinT + ci0) * 2 + (v & 15) * 16) : 0x80000000u, dst + i * 1024);
+      }
+    }
+  };
+  int tile = t_beg, k = 0;
+  if (tile < t_end) issue(tile, 0);
+  for (; tile < t_end; tile++, k++) {
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (tile + 1 < t_end) issue(tile + 1, (k + 1) & 1);
+    const char* dyi = smem + (k & 1) * BUF;
+    const char* hxi = dyi + AB;
+    for (int ty = 0; ty < TH; ty++) {                     // K step = one dy row of 32 pixels
+      bf16x8 fa[NCO];
+#pragma unroll
+      for (int cb = 0; cb < NCO; cb++) fa[cb] = trf(dyi, ty * TW, cb * 16, lane, dy_at<64>);
+#pragma unroll
+      for (int j = 0; j < NP; j++) {
+        const int pr = pair0 + j, tap = pr >> 2, cib = pr & 3, ky = tap >> 2, kx = tap & 3;
+        // halo column 2 k + kx of halo row 2 ty + ky = sub-row (kx & 1), entry k + (kx >> 1)
+        const bf16x8 fb = trf(hxi, ((2 * ty + ky) * 2 + (kx & 1)) * HS + (kx >> 1), cib * 16, lane, hx_at);
+#pragma unroll
+        for (int cb = 0; cb < NCO; cb++) acc[j][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[cb], fb, acc[j][cb], 0, 0, 0);
+      }
+    }
+  }
+  const int g = lane >> 4, li = lane & 15;
+#pragma unroll
+  for (int j = 0; j < NP; j++) {
+    const int pr = pair0 + j, tap = pr >> 2, cib = pr & 3;
+#pragma unroll
+    for (int cb = 0; cb < NCO; cb++)
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        atomicAdd(ws + (long)(co0 + cb * 16 + 4 * g + r) * (16 * CinT) + tap * CinT + ci0 + cib * 16 + li, acc[j][cb][r]);
+  }
+}
+static int launch_wgrad4s2(const bf16* dy, const bf16* x, float* ws, int B, int OH, int OW, int CinT, int CoT, hipStream_t st) {
+  auto kfn = conv4s2_wgrad_dma_kernel;
+  static bool attr = false;
+  if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, wg4::LDS); attr = true; }
+  const int tx = cdiv(OW, wg4::TW), ty = cdiv(OH, wg4::TH);
+  const long tiles = (long)B * tx * ty;
+  if (tiles >= (1L << 31)) { s3od_set_error("wgrad 4s2: too many tiles"); return 22; }
+  static int ncu = 0;
+  if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
+  const int nci = CinT / 64, nblk = (CoT / 64) * nci;
+  const int wpc = (int)std::max<long>(1, std::min<long>(tiles, std::max(1, ncu / nblk)));
+  hipLaunchKernelGGL(kfn, dim3(nblk * wpc), dim3(256), wg4::LDS, st, dy, x, ws, OH, OW, tx, ty, (int)tiles, CinT, CoT, nci, wpc);
+  return s3od_check_launch("conv4s2_wgrad_dma");
+}
+
 // S3OD_WGRAD_DMA=0 (read per call) keeps the register-staged kernel
 template <bool RELU>
 static int launch_wgrad_dma(const bf16* dy, const bf16* x, float* ws, int B, int H, int W, int CinT, int CoT, hipStream_t st) {
@@ -1575,6 +1688,15 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
   // halo-tile kernel: 3x3 s1 p1, Cin a multiple of 64, Cout a multiple of 64 (or 96 for the mask heads).
   // Measured at bs 16 (tools/lin_sweep.py SWEEP=conv64): 2.4x / 1.75x on the 1024^2 64 -> 64 / 96 convs,
   // 1.2x on 512^2 256 -> 128, equal at 256^2 / 128^2 and 8 % slower at 64^2 -> used for Cin 64 or >= 512^2 maps
+  if (dtype == S3OD_BF16 && ws && KH == 4 && KW == 4 && stride == 2 && pad == 1 && H == 2 * OH && W == 2 * OW && Cin % 64 == 0 &&
+      Cout % 64 == 0 && !relu_x && (long)H * W * Cin * 2 < (1L << 31) && (long)OH * OW * Cout * 2 < (1L << 31) &&
+      !getenv_zero("S3OD_WGRAD_DMA")) {
+    // the ConvTranspose2d(128, 64, 4, 2, 1) weight (upsample_2x.0) in its conv view
+    int rc = launch_wgrad4s2((const bf16*)dy, (const bf16*)x, ws, B, OH, OW, Cin, Cout, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(wgrad_permute_add_kernel, dim3(cdiv((long)M * N, 256)), dim3(256), 0, st, ws, dw, M, Cin, KH * KW);
+    return s3od_check_launch("conv_wgrad permute");
+  }
   const int coblk = Cout % 64 == 0 ? 64 : (Cout == 96 ? 96 : 0);
   if (wg_knob && dtype == S3OD_BF16 && ws && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W &&
       Cin % 64 == 0 && coblk && (Cin == 64 || (long)H * W >= 512L * 512)) {

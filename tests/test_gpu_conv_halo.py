@@ -209,3 +209,30 @@ def test_conv_4s2_register_weight_colsum(B, H, W):
         ref_cs = ref.sum((0, 2, 3))
         tol = 2e-3 * ref.abs().sum((0, 2, 3)).max()
         assert float((cs - ref_cs).abs().max()) <= float(tol), (knob, float((cs - ref_cs).abs().max()), float(tol))
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 19, 37), (1, 32, 64), (1, 5, 70)])
+def test_conv_4s2_wgrad(B, H, W):
+    """Weight gradient of the conv view of upsample_2x.0 (4x4, stride 2, pad 1; dy 128 channels on H x W, x 64 channels
+    on 2H x 2W) on the LDS-DMA register-accumulator kernel (conv4s2_wgrad_dma_kernel) and on the implicit GEMM
+    (S3OD_WGRAD_DMA=0) vs torch's conv2d_weight of the same bf16 operands, accumulated into an existing gradient."""
+    import os
+    from s3od_amd._lib import lib, stream
+    g = torch.Generator(device="cuda").manual_seed(H * W + B)
+    dy = torch.randn(B, 128, H, W, device="cuda", generator=g).bfloat16()
+    x = torch.randn(B, 64, 2 * H, 2 * W, device="cuda", generator=g).bfloat16()
+    ref = torch.nn.grad.conv2d_weight(x.float(), (128, 64, 4, 4), dy.float(), stride=2, padding=1)
+    for knob in ("1", "0"):
+        os.environ["S3OD_WGRAD_DMA"] = knob
+        try:
+            dw0 = torch.randn(128, 64, 4, 4, device="cuda", generator=g)
+            dw = dw0.clone()
+            ws = torch.zeros(128 * 16 * 64, device="cuda")
+            lib()("s3od_conv_wgrad", BF16, B, 2 * H, 2 * W, 64, H, W, 128, 4, 4, 2, 1, _nhwc(dy), _nhwc(x), 0, dw, ws, 0,
+                  stream())
+            torch.cuda.synchronize()
+        finally:
+            os.environ.pop("S3OD_WGRAD_DMA", None)
+        assert int((ws != 0).sum()) == 0, "conv_wgrad must leave its workspace all zero"
+        got = dw - dw0
+        assert float((got - ref).abs().max() / ref.abs().max()) < 2e-3, (knob, float((got - ref).abs().max() / ref.abs().max()))

@@ -50,6 +50,27 @@ def main():
         for k in ("1",):
             a = res[k]
             print(f"{H}^2 {k}: max |dma - staged| / max|staged| = {float((a - b).abs().max() / b.abs().max()):.3e}")
+    # upsample_2x.0 (ConvTranspose2d(128, 64, 4, 2, 1)) in its conv view: dy 512^2 x 128, x 1024^2 x 64
+    H = 512
+    g = torch.Generator(device="cuda").manual_seed(7)
+    dy = torch.randn(B, H, H, 128, device="cuda", generator=g).bfloat16()
+    x = torch.randn(B, 2 * H, 2 * H, 64, device="cuda", generator=g).bfloat16()
+    ws = torch.zeros(128 * 16 * 64, device="cuda")
+    fl = 2.0 * B * H * H * 128 * 64 * 16
+    res = {}
+    for rnd in range(3):
+        for knob in ("0", "1"):
+            os.environ["S3OD_WGRAD_DMA"] = knob
+            dw = torch.zeros(128, 64, 4, 4, device="cuda")
+            f = lambda: lib()("s3od_conv_wgrad", BF16, B, 2 * H, 2 * H, 64, H, H, 128, 4, 4, 2, 1, dy, x, 0, dw, ws, 0, stream())
+            t = timeit(f)
+            dw.zero_()
+            f()
+            torch.cuda.synchronize()
+            res[knob] = dw.clone()
+            print(f"convT wgrad 4x4 s2 round {rnd} DMA={knob}: {t * 1e6:8.1f} us {fl / t / 1e12:7.1f} TF/s", flush=True)
+    a, b = res["1"], res["0"]
+    print(f"convT wgrad: max |dma - gemm| / max|gemm| = {float((a - b).abs().max() / b.abs().max()):.3e}")
     os.environ.pop("S3OD_WGRAD_DMA", None)
 
 
