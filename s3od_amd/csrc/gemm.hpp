@@ -903,9 +903,11 @@ template <> struct Row8<bf16> {
 // ------------------------------------------------------------------ common epilogue
 // out = act(acc*scale[n] + shift[n]) + res1 + res2 ; optional raw store (pre-act) and BN
 // batch statistics (sum / sum of squares of the pre-activation value, fp64 atomics).
-enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3, ACT_RELU_BWD = 4 };
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3, ACT_RELU_BWD = 4, ACT_GELU_SG = 5, ACT_MUL = 6 };
 // ACT_GELU_BWD: o = v * gelu'(res1)   (res1 = saved pre-activation, not added)
 // ACT_RELU_BWD: o = v * (res1 > 0)    (res1 = saved activation output, not added)
+// ACT_GELU_SG:  o = gelu(v) and `pre` receives gelu'(v) instead of the pre-activation (one erf serves both)
+// ACT_MUL:      o = v * res1          (res1 = the saved gelu'(v) of ACT_GELU_SG, not added)
 template <typename TO, typename TR, typename TP = TO> struct EpiStd {
   // pre = acc + bias[n] ;  v = pre*scale[n] + shift[n] ;  out = act(v) (+res1 +res2)
   TO* out; long ldo; int coff;          // output row stride / channel offset
@@ -965,7 +967,7 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
 #pragma unroll
         for (int e = 0; e < 8; e++) { pv[e] = a[e] + (bias ? bias[n + e] : 0.f); v[e] = pv[e] * (scale ? scale[n + e] : 1.f) + (shift ? shift[n + e] : 0.f); }
       }
-      if (pre) store8<TP>(pre + orow * ldp + n, pv);
+      if (pre && act != ACT_GELU_SG) store8<TP>(pre + orow * ldp + n, pv);
       // act is uniform: branch once per segment, so the erf path is never speculated for the others
       constexpr bool FAST = sizeof(TP) == 2;     // bf16 compute: branch-free GELU (common.hpp)
       float rp[8];
@@ -983,6 +985,20 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
         float r[8]; if (pf) { for (int e = 0; e < 8; e++) r[e] = rp[e]; } else load8<TR>(res1 + orow * ldr1 + n, r);
 #pragma unroll
         for (int e = 0; e < 8; e++) o[e] = r[e] > 0.f ? v[e] : 0.f;
+      } else if (act == ACT_MUL) {
+        float r[8]; if (pf) { for (int e = 0; e < 8; e++) r[e] = rp[e]; } else load8<TR>(res1 + orow * ldr1 + n, r);
+#pragma unroll
+        for (int e = 0; e < 8; e++) o[e] = v[e] * r[e];
+      } else if (act == ACT_GELU_SG) {
+        float gd[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          float f, ex;
+          erf_as(v[e], f, ex);
+          o[e] = 0.5f * v[e] * (1.0f + f);
+          gd[e] = 0.5f * (1.0f + f) + v[e] * (0.39894228040143268f * ex);
+        }
+        if (pre) store8<TP>(pre + orow * ldp + n, gd);
       } else {
         if (act == ACT_GELU) {
 #pragma unroll

@@ -1408,7 +1408,7 @@ int s3od_linear_fwd(int dtype, int M, int N, int K, const void* x, long ldx, con
       // linears (o_proj 241 -> 215 us, up 576 -> 563, down 487 -> 418); else 256x128 x 3 stages for
       // K >= 2048, 128x128 otherwise
       // (plain bias-only epilogues stay on 128x128: the DPT projections M=65536 N=1024 K=768 157 -> 146 us)
-      const int def = (pp_pays(M, N) && N % 256 == 0 && (res1 || act == ACT_GELU || K >= 2048)) ? 5
+      const int def = (pp_pays(M, N) && N % 256 == 0 && (res1 || act == ACT_GELU || act == ACT_GELU_SG || K >= 2048)) ? 5
                       : (K >= 2048 ? 0 : 1);
       return with_cfg<T>(def, [&](auto C) -> int {
         constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;

@@ -136,3 +136,28 @@ def test_pp_linear_wgrad_split(Nout, Kin, rows):
     ref = dw0 + dy.float().t() @ x.float()
     torch.cuda.synchronize()
     assert rel_l2(dw, ref) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K", [(16384 + 80, 3072, 768), (16384 + 80, 1792, 200)])
+def test_pp_gelu_saved_derivative_pair(M, N, K):
+    """bf16 training's MLP pair: the up-projection with act 5 (ACT_GELU_SG) writes GELU(v) to out and gelu'(v) to pre;
+    the down-projection dgrad with act 6 (ACT_MUL) multiplies dy w by that saved derivative.  Against fp32 torch
+    (gelu and its autograd derivative of the same pre-activation)."""
+    torch.manual_seed(M + N + 1)
+    L, s = _lib()
+    x, w, b = r(M, K), r(N, K, scale=K ** -0.5), r(N, dt=torch.float32)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    gsave = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    L("s3od_linear_fwd", BF16, M, N, K, x, K, w, b, None, None, 5, None, N, None, 0, 0, out, N, 0, gsave, N, 0, 0, 0, s)
+    ref_pre = (x.float() @ w.float().t() + b).requires_grad_(True)
+    ref = torch.nn.functional.gelu(ref_pre)
+    ref_g = torch.autograd.grad(ref.sum(), ref_pre)[0]
+    torch.cuda.synchronize()
+    assert rel_l2(out.float(), ref.detach()) < 5e-3
+    assert rel_l2(gsave.float(), ref_g) < 5e-3
+    Kd = 768
+    dy, wd = r(M, Kd), r(Kd, N, scale=Kd ** -0.5)
+    dx = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    L("s3od_linear_dgrad", BF16, M, N, Kd, dy, Kd, wd, 6, gsave, N, dx, N, 0, 0, 0, 0, None, s)
+    torch.cuda.synchronize()
+    assert rel_l2(dx.float(), (dy.float() @ wd.float()) * ref_g) < 6e-3

@@ -85,6 +85,8 @@ def main():
         " * parity path, v_mfma_f32_16x16x4_f32), 1 = bf16 (fast path, v_mfma_f32_16x16x32_bf16).",
         " * Activations are NHWC; weights are repacked [Cout][KH][KW][Cin] for the kernels while",
         " * gradients are written in the reference (PyTorch state_dict) layout.",
+        " * act (GEMM / conv epilogues): 0 none, 1 ReLU, 2 GELU (erf), 3 x GELU'(res1 = saved pre-activation),",
+        " * 4 x ReLU'(res1 = saved output), 5 GELU with gelu'(v) written to `pre`, 6 x res1 (a saved gelu').",
         " * Return: 0 on success, otherwise a hipError_t or 22 (invalid argument);",
         " * s3od_last_error() describes the last failure on the calling thread.",
         " */",

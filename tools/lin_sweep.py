@@ -118,6 +118,13 @@ if __name__ == "__main__":
         wgrad_conv("conv wgrad 96x(3x3x64) @1024^2 bs16", 16, 1024, 64, 96)
         wgrad_conv("conv wgrad 256x(3x3x256) @256^2 bs16", 16, 256, 256, 256)
         wgrad_conv("conv wgrad 128x(3x3x256) @512^2 bs16", 16, 512, 256, 128)
+        sys.exit(0)
+    if os.environ.get("SWEEP") == "gelu":
+        # the MLP's GELU pair: pre-activation saved + GELU' in the down dgrad, vs gelu'(v) saved + a multiply
+        fwd("up fwd N3072 K768 (GELU, pre saved)", 3072, 768, act=ACT_GELU, pre=True)
+        fwd("up fwd N3072 K768 (GELU, gelu' saved)", 3072, 768, act=5, pre=True)
+        dgrad("down dgrad N3072 K768 (GELU')", 3072, 768, act=ACT_GELU_BWD, aux=True)
+        dgrad("down dgrad N3072 K768 (x saved gelu')", 3072, 768, act=6, aux=True)
         wgrad_conv("conv wgrad 256x(3x3x256) @128^2 bs16", 16, 128, 256, 256)
         wgrad_conv("conv wgrad 256x(3x3x1024) @64^2 bs16", 16, 64, 1024, 256)
         wgrad_conv("conv wgrad 256x(3x3x256) @64^2 bs16", 16, 64, 256, 256)
