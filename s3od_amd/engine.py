@@ -13,6 +13,7 @@ Reference structure: src/s3od/model.py:62-467 and tf:models/dinov3_vit/modeling_
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -23,7 +24,9 @@ from .weights import OUT_CH, VARIANTS
 NREG = 4
 ACT_NONE, ACT_RELU, ACT_GELU, ACT_GELU_BWD, ACT_RELU_BWD = 0, 1, 2, 3, 4
 # bf16 training: the up-projection saves gelu'(v) (one erf for both outputs) and the down dgrad multiplies by it
+# (S3OD_GELU_SG=0: the pre-activation + GELU' form, for A/B runs)
 ACT_GELU_SG, ACT_MUL = 5, 6
+_GELU_SG = os.environ.get("S3OD_GELU_SG", "1") != "0"
 
 
 def _E(ref, n, dt, dev):
@@ -282,7 +285,7 @@ class DPTEngine:
                       scale=P[p + "layer_scale1.lambda1"], res1=xs, res_f32=True, out_f32=True, pre=u1)
             L("s3od_layernorm_fwd", dt, xm, P[p + "norm2.weight"], P[p + "norm2.bias"], h2, mean2, rstd2, M, D, 1e-5, st)
             self._lin(h2, W8[f"up{i}"], M, MLP, D, a, bias=P[p + "mlp.up_proj.bias"],
-                      act=ACT_GELU_SG if (hpre is not None and dt == BF16) else ACT_GELU, pre=hpre)
+                      act=ACT_GELU_SG if (hpre is not None and dt == BF16 and _GELU_SG) else ACT_GELU, pre=hpre)
             xn = _E(None, (B, Nt, D), torch.float32, dev)
             self._lin(a, W8[f"down{i}"], M, D, MLP, xn, bias=P[p + "mlp.down_proj.bias"],
                       scale=P[p + "layer_scale2.lambda1"], res1=xm, res_f32=True, out_f32=True, pre=u2)
@@ -622,7 +625,7 @@ class DPTEngine:
             L("s3od_layerscale_bwd", dt, dx, s["u2"], P[p + "layer_scale2.lambda1"], du, G[p + "layer_scale2.lambda1"],
               G[p + "mlp.down_proj.bias"], red_ws, M, D, st)
             self._wgrad_lin(du, s["a"], D, MLP, M, G[p + "mlp.down_proj.weight"])
-            self._dgrad_lin(du, W8[f"down{i}"], M, MLP, D, dhp, act=ACT_MUL if dt == BF16 else ACT_GELU_BWD, aux=s["hpre"],
+            self._dgrad_lin(du, W8[f"down{i}"], M, MLP, D, dhp, act=ACT_MUL if (dt == BF16 and _GELU_SG) else ACT_GELU_BWD, aux=s["hpre"],
                             colsum=G[p + "mlp.up_proj.bias"])
             self._wgrad_lin(dhp, s["h2"], MLP, D, M, G[p + "mlp.up_proj.weight"])
             self._dgrad_lin(dhp, W8[f"up{i}"], M, D, MLP, dh)
