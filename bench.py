@@ -18,7 +18,7 @@ host's cores (rank 0, N=1 only): 1 warm-up + --cpu-iters (3) timed iterations of
 "CPU-baseline plan": 1 + >= 3), for the train step and for C2 (the `infer` object); the C5 baseline in
 `infer_2048` is one timed 2048^2 image without warm-up (~80 s of CPU per image on the box's share).
 `c1`: configs[0], `BackgroundRemoval.remove_background` on the reference's fixture image end to end (host
-image in, RemovalResult out) beside the oracle's CPU restatement of the same pipeline (1 + 2 iterations).
+image in, RemovalResult out) beside the oracle's CPU restatement of the same pipeline (1 + --cpu-iters iterations).
 Attention backward work follows SURVEY §8(d) (8*N^2*64 per (b,h), recompute not counted); the roofline
 object also carries the executed figure (14*N^2*64) for that entry.
 """
@@ -131,7 +131,17 @@ def cpu_baseline(S, mode, iters, warmup=1):
             "kind": "port", "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count(),
             "iter_s": [round(t, 3) for t in ts],
             "sample": f"1 image {S}x{S}, {what}, fp32 oracle (oracle/s3od_oracle.py), {warmup} warm-up + {iters} timed "
-                      f"iterations, {threads} threads"}
+                      f"iterations, {threads} threads",
+            "deviation": f"the oracle is a restatement, not the reference's executed path: like the GPU engine it skips the "
+                         f"encoder layers past the last tap and the final LayerNorm, whose outputs the reference computes and "
+                         f"discards ({_skipped_note(S)}); threads = the job's CPU share ({threads}), not os.cpu_count() "
+                         f"({os.cpu_count()}) as BASELINE.md:76 says"}
+
+
+def _skipped_note(S):
+    if S == 1024:
+        return "2.2768 of the reference's 2.3865 TF per 1024^2 forward, -4.6 %"
+    return "layer 11 + final norm of dinob, about 4.6 % of the forward"
 
 
 # ------------------------------------------------------------------------------------ profiling helpers
@@ -289,7 +299,10 @@ def c1_plumbing(dev, cpu_iters, steps=10, warmup=2):
             out["cpu_baseline"] = {"value": round(1.0 / ct, 5), "unit": "images/s", "cores": threads, "kind": "port",
                                    "iter_s": [round(t, 3) for t in ts],
                                    "sample": f"the fixture through the oracle's remove_background pieces (fp32), 1 warm-up + "
-                                             f"{cpu_iters} timed, {threads} threads"}
+                                             f"{cpu_iters} timed, {threads} threads",
+                                   "deviation": f"restatement: skips the encoder layers past the last tap and the final "
+                                                f"LayerNorm ({_skipped_note(1024)}); {threads} threads of os.cpu_count() "
+                                                f"{os.cpu_count()}"}
         except Exception as e:  # reported, never fatal for the GPU number
             out["cpu_baseline"] = {"value": None, "error": repr(e)[:200]}
     return out
@@ -363,6 +376,8 @@ def main():
     use_dist = world > 1 or args.ddp
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if use_dist and "RANK" not in os.environ:       # --ddp rehearsal without a launcher: a world of one
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     if use_dist:
         dist.init_process_group("nccl", device_id=dev, timeout=__import__("datetime").timedelta(seconds=int(os.environ.get("S3OD_RCCL_TIMEOUT_S", "1800"))))
 
@@ -374,10 +389,11 @@ def main():
     B = args.batch or (16 if args.mode == "train" else 8)
     S = args.size
     model = DPTSegmentation(compute_dtype=args.dtype).to(dev)
+    sync = None
     if use_dist:
         from s3od_amd.ddp import GradSync, broadcast_parameters
         broadcast_parameters(model)
-        GradSync(model)
+        sync = GradSync(model)
     x, masks = synthetic_batch(B, S, 1000 + rank, dev)
 
     if args.mode == "train":
@@ -414,6 +430,8 @@ def main():
     lib = _lib.lib()
     lib.cost = cost
     lib.timers = {dom: []}
+    if sync is not None:
+        sync.reset_timing(True)
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -431,6 +449,15 @@ def main():
     timers = lib.timers
     lib.timers = {}
     rec = _drain(timers)
+    comm = None
+    if sync is not None:
+        comm = sync.timing_report()
+        sync.reset_timing(False)
+        if comm is not None and world > 1:
+            t = torch.tensor([comm["comm_exposed_ms"], comm["allreduce_ms_per_step"]], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            comm["comm_exposed_ms_max_over_ranks"], comm["allreduce_ms_per_step_max_over_ranks"] = \
+                round(float(t[0]), 3), round(float(t[1]), 3)
     kms = sum(r[1] for r in rec) / max(len(rec), 1)
     work = sum(r[3] for r in rec) / max(len(rec), 1)
     kind = rec[0][2] if rec else "mfma"
@@ -474,6 +501,13 @@ def main():
             ex = work * 14.0 / 8.0
             res["roofline"]["executed_work_per_launch"] = ex
             res["roofline"]["executed_frac"] = round(ex / (kms * 1e-3) / pk, 4)
+        if use_dist:
+            res["comm"] = dict(comm or {}, backend=dist.get_backend(),
+                               rccl_version=".".join(map(str, torch.cuda.nccl.version())) if hasattr(torch.cuda, "nccl") else None,
+                               channels={k: os.environ[k] for k in ("NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS") if k in os.environ}
+                               or "RCCL default (NCCL_MIN/MAX_NCHANNELS unset)",
+                               note="HIP events: per-bucket all-reduce on the comm stream; comm_exposed_ms = the compute "
+                                    "stream's wait from backward end to GradSync.finish()'s join, per step")
         if bd is not None:
             res["breakdown"] = bd
         if args.mode == "train" and world == 1 and not args.no_infer and args.dtype == "bf16":
@@ -484,7 +518,7 @@ def main():
             res["infer_2048"] = dict(infer_rate(model, 4, 2048, 4, 2, dev, ci),
                                      config="high-res 2048x2048 eval forward bs=4 (configs[4])")
             try:
-                res["c1"] = c1_plumbing(dev, min(ci, 2))
+                res["c1"] = c1_plumbing(dev, ci)
             except Exception as e:  # reported, never fatal for the headline number
                 res["c1"] = {"value": None, "error": repr(e)[:200]}
         if not args.no_cpu_baseline and world == 1:

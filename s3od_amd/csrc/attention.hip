@@ -1206,145 +1206,16 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __res
 // (hipcc 7.2 left the host stubs of these instances undefined when they were only named in the launcher below)
 template __global__ void attn_bwd_dq32_kernel<4, false, false, true>(const bf16*, const bf16*, const bf16*, const bf16*, const float*,
                                                                      const float*, bf16*, int, int, QkvSink);
-template __global__ void attn_bwd_dq32_kernel<8, false, false, true>(const bf16*, const bf16*, const bf16*, const bf16*, const float*,
-                                                                     const float*, bf16*, int, int, QkvSink);
 template __global__ void attn_bwd_dkdv32_kernel<4, false, false, true>(const bf16*, const bf16*, const bf16*, const bf16*, const float*,
                                                                        const float*, bf16*, bf16*, int, int, QkvSink);
-template __global__ void attn_bwd_dkdv32_kernel<8, false, false, true>(const bf16*, const bf16*, const bf16*, const bf16*, const float*,
-                                                                       const float*, bf16*, bf16*, int, int, QkvSink);
-
-// ===================================================================================== forward, bf16, 32x32x16
-// Same algorithm as attn_fwd_kernel (swapped products, lazy rescale with the running max in the S MFMA's C
-// operand, row sums from the matrix core) on v_mfma_f32_32x32x16_bf16, whose 32-cycle issue leaves 1.5x the
-// VALU room per multiply-add of the 16x16x32 form for the exp2 / max / pack work.  One wave = 32 queries (the
-// lane's query = lane & 31; the two lane halves hold alternate key rows of the same query), K / V tiles of 64
-// keys by LDS-DMA into Img32 images, one barrier per tile.
-//   S^T[key][q] = K Q^T - m   (A = K rows, B = Q fragments in registers, C = -m of the lane's query)
-//   O^T[d][q]  += V^T P^T     (A = V^T by transposed reads, B = P^T straight from the S accumulators)
-//   l          += 1^T P^T     (one MFMA per 16 keys)
-template <int W>
-__global__ void __launch_bounds__(64 * W) attn_fwd32_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
-                                                              const bf16* __restrict__ V, bf16* __restrict__ O,
-                                                              float* __restrict__ LSE, int N, int H) {
-  constexpr int SB = 2 * Img32::BYTES;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * SB];
-  const int bh = blockIdx.y, b = bh / H, hh = bh - b * H;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5;
-  const auto rk = attn_rsrc(K + (long)bh * N * 64, (unsigned long)N * 128);
-  const auto rv = attn_rsrc(V + (long)bh * N * 64, (unsigned long)N * 128);
-  const int q0 = blockIdx.x * (32 * W) + wave * 32, q = q0 + (lane & 31);
-  bf16x8 qf[4];
-  {
-    const bf16* qr = Q + ((long)bh * N + q) * 64 + 8 * h;
-    bf16x8 z; for (int e = 0; e < 8; e++) z[e] = (bf16)0.f;
-#pragma unroll
-    for (int ks = 0; ks < 4; ks++) qf[ks] = q < N ? *(const bf16x8*)(qr + 16 * ks) : z;
-  }
-  bf16x8 ones;
-#pragma unroll
-  for (int e = 0; e < 8; e++) ones[e] = (bf16)1.f;
-  f32x16 o[2], lacc, negm;
-#pragma unroll
-  for (int i = 0; i < 16; i++) { o[0][i] = 0.f; o[1][i] = 0.f; lacc[i] = 0.f; negm[i] = 0.f; }
-  float mrow = -INFINITY;
-  const int nkt = (N + 63) / 64;
-  auto stage = [&](int kt, char* base) {
-    Dma64<W>::issue(rk, (long)kt * 64, 128, base, wave, lane);
-    Dma64<W>::issue(rv, (long)kt * 64, 128, base + Img32::BYTES, wave, lane);
-  };
-  stage(0, smem);
-  __syncthreads();
-  int cur = 0;
-  for (int kt = 0; kt < nkt; kt++) {
-    if (kt + 1 < nkt) stage(kt + 1, smem + (cur ^ 1) * SB);
-    const char* ks_ = smem + cur * SB;
-    const char* vs_ = ks_ + Img32::BYTES;
-    f32x16 s[2];
-#pragma unroll
-    for (int kb = 0; kb < 2; kb++) {
-      bf16x8 a[4];
-#pragma unroll
-      for (int ks = 0; ks < 4; ks++) a[ks] = row32(ks_, 32 * kb, ks, lane);
-      s[kb] = mma32(a[0], qf[0], negm);
-#pragma unroll
-      for (int ks = 1; ks < 4; ks++) s[kb] = mma32(a[ks], qf[ks], s[kb]);
-    }
-    if (kt * 64 + 64 > N) {   // keys >= N (last tile only)
-#pragma unroll
-      for (int kb = 0; kb < 2; kb++)
-#pragma unroll
-        for (int i = 0; i < 16; i++)
-          if (kt * 64 + 32 * kb + acc_row(i, h) >= N) s[kb][i] = -INFINITY;
-    }
-    // lazy max: s holds score - m; the first tile sets m, later tiles rescale only when a score exceeds m
-    // by more than RESCALE_TH (wave-uniform branch)
-    float lm = -INFINITY;
-#pragma unroll
-    for (int kb = 0; kb < 2; kb++)
-#pragma unroll
-      for (int i = 0; i < 16; i += 2) lm = fmaxf(lm, fmaxf(s[kb][i], s[kb][i + 1]));
-    if (kt == 0 || __any(lm > RESCALE_TH)) {
-      float d = fmaxf(lm, __shfl_xor(lm, 32));
-      d = kt == 0 ? d : fmaxf(d, 0.f);
-      mrow = kt == 0 ? d : mrow + d;
-      const float alpha = kt == 0 ? 1.f : fexp2(-d);
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        s[0][i] -= d; s[1][i] -= d;
-        o[0][i] *= alpha; o[1][i] *= alpha; lacc[i] *= alpha;
-        negm[i] = -mrow;
-      }
-    }
-    // P = exp2(s);  O^T += V^T P^T;  l += 1^T P^T   (k = key: 4 steps of 16)
-#pragma unroll
-    for (int kb = 0; kb < 2; kb++) {
-#pragma unroll
-      for (int i = 0; i < 16; i++) s[kb][i] = fexp2(s[kb][i]);
-#pragma unroll
-      for (int st = 0; st < 2; st++) {
-        const bf16x8 pb = pack_acc(s[kb], st);
-        bf16x8 va[2];
-#pragma unroll
-        for (int db = 0; db < 2; db++) va[db] = tr32(vs_, 32 * kb + 16 * st, 32 * db, lane);
-#pragma unroll
-        for (int db = 0; db < 2; db++) o[db] = mma32(va[db], pb, o[db]);
-        lacc = mma32(ones, pb, lacc);
-      }
-    }
-    __syncthreads();
-    cur ^= 1;
-  }
-  // epilogue: O[b][q][hh*64 + d], d = 32 db + acc_row(i, h) (4 consecutive d per register group);
-  // LSE (log2 units) = m + log2(l)
-  if (q < N) {
-    const float l = lacc[0], inv = 1.0f / l;
-    bf16* orow = O + ((long)b * N + q) * (H * 64) + hh * 64;
-#pragma unroll
-    for (int db = 0; db < 2; db++)
-#pragma unroll
-      for (int m4 = 0; m4 < 4; m4++) {
-        const int d = 32 * db + 8 * m4 + 4 * h;
-        bf16x4 v = {(bf16)(o[db][4 * m4] * inv), (bf16)(o[db][4 * m4 + 1] * inv), (bf16)(o[db][4 * m4 + 2] * inv),
-                    (bf16)(o[db][4 * m4 + 3] * inv)};
-        *(bf16x4*)(orow + d) = v;
-      }
-    if (h == 0 && LSE) LSE[(long)bh * N + q] = mrow + __log2f(l);
-  }
-}
 
 extern "C" {
 
 // q,k,v: [B*H, N, 64] (q pre-scaled by log2(e)/8); o: [B, N, H*64]; lse: [B*H, N] fp32, log2 units (optional)
 int s3od_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* o, float* lse, int B, int H, int N, void* stream) {
   dim3 grid(cdiv(N, 128), B * H);
-  // bf16: the 16x16x32 kernel; the 32x32x16 one (S3OD_ATTN_FWD=32) measured 6-8 % slower (1083 -> 1150 us at
-  // bs 16, N 4101; 3532 -> 3817 us at bs 4, N 16389, same box): its extra row-sum MFMAs cost 2x the cycles
-  static const int fwd32 = dev_knob("S3OD_ATTN_FWD", 16) == 32;
-  if (dtype == S3OD_BF16 && fwd32) {
-    hipLaunchKernelGGL((attn_fwd32_kernel<4>), grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)q, (const bf16*)k,
-                       (const bf16*)v, (bf16*)o, lse, N, H);
-    return s3od_check_launch("attn_fwd");
-  }
+  // bf16 and f32: the 16x16 kernel (a 32x32x16 bf16 variant measured 6-8 % slower: 1083 -> 1150 us at bs 16, N 4101;
+  // 3532 -> 3817 us at bs 4, N 16389, same box -- its extra row-sum MFMAs cost 2x the cycles; removed)
   DISPATCH_T(dtype, {
     hipLaunchKernelGGL(attn_fwd_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, N, H);
   });
@@ -1353,12 +1224,6 @@ int s3od_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* 
 }  // extern "C"
 
 namespace {
-// bf16 backward body: 1 = 32x32x16 kernels (default), 0 = the 16x16x32 kernels (S3OD_ATTN_BWD=16 selects them,
-// for A/B measurement)
-int attn_bwd_variant() {
-  static int v = [] { const char* e = getenv("S3OD_ATTN_BWD"); return (e && e[0] == '1' && e[1] == '6') ? 0 : 1; }();
-  return v;
-}
 __global__ void qkv_fold_kernel(float* __restrict__ ws, float* __restrict__ a, float* __restrict__ b, int D) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 2 * D) return;
@@ -1375,43 +1240,20 @@ void launch_bwd(const void* q, const void* k, const void* v, const void* o, cons
   // needs > 256 registers -> one wave per SIMD: the whole backward measured 19 % (dK/dV) / 11 % (dQ) slower at N=4101
   hipLaunchKernelGGL(attn_delta_kernel<T>, dim3(cdiv((long)B * H * N * 8, 256)), dim3(256), 0, st, (const T*)o, (const T*)dout, delta, N, H, B * H);
   if constexpr (std::is_same<T, bf16>::value) {
-    if (attn_bwd_variant() == 1) {
-      // waves per workgroup (dev knobs for A/B: S3OD_ATTN_WK for the dK/dV pass, S3OD_ATTN_WQ for the dQ pass)
-      static const int wk = dev_knob("S3OD_ATTN_WK", 4), wq = dev_knob("S3OD_ATTN_WQ", 4), pr = dev_knob("S3OD_ATTN_PRIO", 0),
-                            il = dev_knob("S3OD_ATTN_IL", 0), u2 = dev_knob("S3OD_ATTN_U2", 1);
-      auto go_kv = [&](auto w) {
-        constexpr int W = decltype(w)::value;
-        if (u2) hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<W, false, false, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st,
-                                   (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv,
-                                   N, H, sink);
-        else if (pr) hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<W, true, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st, (const bf16*)q,
-                                   (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv, N, H, sink);
-        else if (il) hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<W, false, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st,
-                                        (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv,
-                                        N, H, sink);
-        else hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<W, false, false>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st, (const bf16*)q,
-                           (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv, N, H, sink);
-      };
-      auto go_q = [&](auto w) {
-        constexpr int W = decltype(w)::value;
-        if (u2) hipLaunchKernelGGL((attn_bwd_dq32_kernel<W, false, false, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st,
-                                   (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, N, H, sink);
-        else if (pr) hipLaunchKernelGGL((attn_bwd_dq32_kernel<W, true, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st, (const bf16*)q,
-                                   (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, N, H, sink);
-        else if (il) hipLaunchKernelGGL((attn_bwd_dq32_kernel<W, false, true>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st,
-                                        (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, N, H, sink);
-        else hipLaunchKernelGGL((attn_bwd_dq32_kernel<W, false, false>), dim3(cdiv(N, 32 * W), B * H), dim3(64 * W), 0, st, (const bf16*)q,
-                           (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, N, H, sink);
-      };
-      if (wk == 8) go_kv(std::integral_constant<int, 8>{}); else go_kv(std::integral_constant<int, 4>{});
-      if (wq == 8) go_q(std::integral_constant<int, 8>{}); else go_q(std::integral_constant<int, 4>{});
-      return;
-    }
+    // bf16: the 32x32x16 kernels, 4 waves per workgroup, tile loops unrolled by two (the 16x16x32 bf16 bodies,
+    // 8-wave workgroups, s_setprio and interleaved variants were measured slower and removed: DESIGN §6)
+    hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<4, false, false, true>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st,
+                       (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv, N, H,
+                       sink);
+    hipLaunchKernelGGL((attn_bwd_dq32_kernel<4, false, false, true>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st,
+                       (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, N, H, sink);
+    return;
+  } else {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, 2>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v,
+                       (const T*)dout, lse, delta, (T*)dk, (T*)dv, N, H, sink);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<T, 2>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v,
+                       (const T*)dout, lse, delta, (T*)dq, N, H, sink);
   }
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<T, 2>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v,
-                     (const T*)dout, lse, delta, (T*)dk, (T*)dv, N, H, sink);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<T, 2>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v,
-                     (const T*)dout, lse, delta, (T*)dq, N, H, sink);
 }
 }  // namespace
 

@@ -69,14 +69,20 @@ __global__ void bn_fold_kernel(const float* w, const float* b, const float* rm, 
 
 // train: stats = (sum, sumsq) over count values of z = conv + bias. Writes mean/rstd (for backward),
 // scale/shift (for apply) and updates running stats (momentum, unbiased var) like nn.BatchNorm2d.
-// stats enter as the conv epilogue's fp64 [sum | sum of squares] and are cleared here (persistent workspace)
+// stats enter as the conv epilogue's fp64 [S3OD_NREP][sum | sum of squares] replicas and are folded and cleared
+// here (persistent workspace)
 __global__ void bn_finalize_kernel(double* stats, long count, const float* w, const float* b, float* rm, float* rv,
                                    float momentum, float eps, float* mean_o, float* rstd_o, float* scale, float* shift, int C) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  double mean = stats[c] / (double)count;
-  double var = stats[C + c] / (double)count - mean * mean;
-  stats[c] = 0.0; stats[C + c] = 0.0;
+  double s1 = 0.0, s2 = 0.0;
+  for (int r = 0; r < S3OD_NREP; r++) {
+    double* st = stats + (long)r * 2 * C;
+    s1 += st[c]; s2 += st[C + c];
+    st[c] = 0.0; st[C + c] = 0.0;
+  }
+  double mean = s1 / (double)count;
+  double var = s2 / (double)count - mean * mean;
   if (var < 0) var = 0;
   float rstd = (float)(1.0 / sqrt(var + (double)eps));
   mean_o[c] = (float)mean; rstd_o[c] = rstd;
@@ -566,6 +572,7 @@ int s3od_bn_fold(const float* w, const float* b, const float* rm, const float* r
   return s3od_check_launch("bn_fold");
 }
 
+// stats: [S3OD_NREP][2][C] fp64 replicas of the conv epilogue's (sum, sum of squares) of z, folded and left all zero
 int s3od_bn_finalize(double* stats, long count, const float* w, const float* b, float* rm, float* rv, float momentum,
                      float eps, float* mean, float* rstd, float* scale, float* shift, int C, void* stream) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, stats, count, w, b, rm, rv,

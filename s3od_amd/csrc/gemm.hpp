@@ -59,35 +59,26 @@ static inline ConvGeo make_class(ConvGeo g, int OH, int OW, int py, int px) {
 
 // maps a GEMM row m to the linear output-pixel (row) index of the stored tensor
 struct RowMap {
-  int mode;          // 0 dense, 1 tokens (skip prefix), 2 parity class, 3 spatial tiles
+  int mode;          // 0 dense, 1 tokens (skip prefix), 2 parity class
   int P, prefix;     // tokens: m = b*P + p -> b*(P+prefix) + prefix + p
   int RH, RW, OH, OW, s, py, px;   // class: (b,y',x') -> (b, py+s*y', px+s*x') in OH x OW
-                                   // tiles: RH x RW tiles of TH x TW pixels (TH = s, TW = py) over OH x OW;
-                                   //   m = tile*TH*TW + ty*TW + tx -> pixel, or -1 outside the image
   DEV long map(int m) const {
     if (mode == 0) return m;
     if (mode == 1) { int b = m / P; return (long)b * (P + prefix) + prefix + (m - b * P); }
-    if (mode == 3) {
-      const int per = s * py, tile = m / per, r = m - tile * per;
-      const int txi = tile % RW, t2 = tile / RW, tyi = t2 % RH, b = t2 / RH;
-      const int y = tyi * s + r / py, x = txi * py + r % py;
-      return (y < OH && x < OW) ? ((long)b * OH + y) * OW + x : -1;
-    }
     int hw = RH * RW; int b = m / hw; int r = m - b * hw; int yy = r / RW; int xx = r - yy * RW;
     return ((long)b * OH + (py + s * yy)) * OW + (px + s * xx);
   }
 };
 
+// ReLU of two packed bf16: a bf16 with the sign bit set is a negative int16, so a signed 16-bit max against
+// 0 is ReLU (-0 -> +0) -- one v_pk_max_i16 per dword instead of a mask / select sequence
+typedef short s16x2_t __attribute__((ext_vector_type(2)));
+DEV unsigned relu_bf16x2(unsigned x) {
+  return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(s16x2_t, x), (s16x2_t){0, 0}));
+}
 template <typename T> DEV uint4 relu16(uint4 v) {
   if constexpr (sizeof(T) == 2) {
-    unsigned w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      unsigned lo = (w[i] & 0x8000u) ? 0u : (w[i] & 0xFFFFu);
-      unsigned hi = (w[i] & 0x80000000u) ? 0u : (w[i] & 0xFFFF0000u);
-      w[i] = lo | hi;
-    }
-    return make_uint4(w[0], w[1], w[2], w[3]);
+    return make_uint4(relu_bf16x2(v.x), relu_bf16x2(v.y), relu_bf16x2(v.z), relu_bf16x2(v.w));
   } else {
     float4 f = *(float4*)&v;
     f.x = fmaxf(f.x, 0.f); f.y = fmaxf(f.y, 0.f); f.z = fmaxf(f.z, 0.f); f.w = fmaxf(f.w, 0.f);
@@ -122,19 +113,12 @@ DEV void blds16(__amdgpu_buffer_rsrc_t r, unsigned voff, char* lds_wave_base) {
 }
 DEV int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
-// Where a loader's 16-B-per-lane chunk i goes.  Every loader computes one buffer offset per chunk
-// (source-side swizzle, OOB -> zeros) and hands it to a sink:
-//   DmaSink  LDS-DMA straight into the lane-linear LDS image (buffer_load_dwordx4 ... lds)
-//   RegSink  buffer_load_dwordx4 into registers; commit() later writes them to the same LDS
-//            positions with ds_write_b128 (register staging: no LDS-DMA issue cost per KiB)
-typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+// Where a loader's 16-B-per-lane chunk i goes: every loader computes one buffer offset per chunk (source-side
+// swizzle, OOB -> zeros) and hands it to the sink, which LDS-DMAs it straight into the lane-linear LDS image
+// (buffer_load_dwordx4 ... lds).
 struct DmaSink {
   char* base;                                    // tile + wave * NIW * 1024
   DEV void operator()(int i, __amdgpu_buffer_rsrc_t r, unsigned voff) const { blds16(r, voff, base + i * 1024); }
-};
-struct RegSink {
-  u32x4_t* regs;
-  DEV void operator()(int i, __amdgpu_buffer_rsrc_t r, unsigned voff) const { regs[i] = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0); }
 };
 #define HD __host__ __device__
 
@@ -183,13 +167,6 @@ template <typename T, int R, int NW = GEMM_WAVES> struct DenseKC {          // X
     }
   }
   DEV void issue(int kt, char* tile) { issue_to(kt, DmaSink{tile + wave_id() * NIW * 1024}); }
-  // register staging: chunk i of this lane -> regs[i]; commit(tile, regs) stores it to LDS
-  DEV void issue_regs(int kt, u32x4_t* regs) { issue_to(kt, RegSink{regs}); }
-  DEV void commit(char* tile, const u32x4_t* regs) const {
-    char* b = tile + wave_id() * NIW * 1024 + (threadIdx.x & 63) * 16;
-#pragma unroll
-    for (int i = 0; i < NIW; i++) *(u32x4_t*)(b + i * 1024) = regs[i];
-  }
   template <class SK> DEV void issue_to(int kt, SK sk) {
     const auto rs = make_rsrc(pb, nb);
     const unsigned adv = (unsigned)(kt * BK * sizeof(T));
@@ -202,65 +179,6 @@ template <typename T, int R, int NW = GEMM_WAVES> struct DenseKC {          // X
     for (int i = 0; i < NIW; i++) sk(i, rs, vo[i] + adv);
   }
 };
-
-// LayerNorm fused into a GEMM's A operand (north_star "fused LayerNorm+QKV projection", measurement
-// prototype): A[row][k] = bf16((x[row][k] - mean[row]) * rstd[row] * g[k] + b[k]) from the fp32 residual
-// stream, REGISTER staged (LDS-DMA cannot transform): issue_regs loads this lane's 8 fp32 of each chunk,
-// commit normalises them and writes the bf16 chunk to the same LDS position the DMA path would.
-template <int R, int NW = GEMM_WAVES> struct LnA {
-  static constexpr int ROWS = R;
-  static constexpr bool KCL = true, RELU = false, REG = true;
-  typedef KCGeom<bf16, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
-  const float* x; long ld; int nrows, K;
-  const float* mean; const float* rstd; const float* g; const float* b;
-  const float* xb; unsigned long nb;
-  unsigned vo[NIW]; int kel[NIW]; float mu[NIW], rs[NIW];
-  HD bool buf_ok() const { return ((unsigned long)(R - 1) * ld + K) * 4 < BUF_MAX; }
-  DEV void setup(int t0, int tid) {
-    const int lane = tid & 63, wave = wave_id();
-    const int rem = nrows - t0;
-    xb = x + (long)t0 * ld;
-    nb = rem > 0 ? ((unsigned long)(min(rem, R) - 1) * ld + K) * 4 : 0;
-#pragma unroll
-    for (int i = 0; i < NIW; i++) {
-      const int r = G::row(wave, i, lane);
-      kel[i] = G::kel(wave, i, lane);
-      vo[i] = r < rem ? (unsigned)(((long)r * ld + kel[i]) * 4) : BUF_OOB;
-      mu[i] = r < rem ? mean[t0 + r] : 0.f;
-      rs[i] = r < rem ? rstd[t0 + r] : 0.f;
-    }
-  }
-  DEV void issue(int, char*) {}                    // (register-staged only)
-  DEV void issue_regs(int kt, u32x4_t* regs) {     // 2 x 16 B of fp32 per chunk
-    const auto rs_ = make_rsrc(xb, nb);
-    const unsigned adv = (unsigned)(kt * BK * 4);
-#pragma unroll
-    for (int i = 0; i < NIW; i++) {
-      regs[2 * i] = __builtin_amdgcn_raw_buffer_load_b128(rs_, vo[i] + adv, 0, 0);
-      regs[2 * i + 1] = __builtin_amdgcn_raw_buffer_load_b128(rs_, vo[i] + adv + 16, 0, 0);
-    }
-  }
-  DEV void commit(char* tile, const u32x4_t* regs, int kt) const {
-    char* base = tile + wave_id() * NIW * 1024 + (threadIdx.x & 63) * 16;
-#pragma unroll
-    for (int i = 0; i < NIW; i++) {
-      const int k = kt * BK + kel[i];
-      const float4 g0 = *(const float4*)(g + k), g1 = *(const float4*)(g + k + 4);
-      const float4 b0 = *(const float4*)(b + k), b1 = *(const float4*)(b + k + 4);
-      const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-      const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-      bf16x8 o;
-#pragma unroll
-      for (int e = 0; e < 8; e++) {
-        const float xv = __uint_as_float(regs[2 * i + (e >> 2)][e & 3]);
-        o[e] = (bf16)((xv - mu[i]) * rs[i] * gv[e] + bv[e]);
-      }
-      *(bf16x8*)(base + i * 1024) = o;
-    }
-  }
-};
-template <class L> struct IsReg { static constexpr bool v = false; };
-template <int R, int NW> struct IsReg<LnA<R, NW>> { static constexpr bool v = true; };
 
 template <typename T, int R, int NW = GEMM_WAVES> struct DenseMC {          // X[k*ld + col]
   static constexpr int ROWS = R;
@@ -284,13 +202,6 @@ template <typename T, int R, int NW = GEMM_WAVES> struct DenseMC {          // X
     }
   }
   DEV void issue(int kt, char* tile) { issue_to(kt, DmaSink{tile + wave_id() * NIW * 1024}); }
-  // register staging: chunk i of this lane -> regs[i]; commit(tile, regs) stores it to LDS
-  DEV void issue_regs(int kt, u32x4_t* regs) { issue_to(kt, RegSink{regs}); }
-  DEV void commit(char* tile, const u32x4_t* regs) const {
-    char* b = tile + wave_id() * NIW * 1024 + (threadIdx.x & 63) * 16;
-#pragma unroll
-    for (int i = 0; i < NIW; i++) *(u32x4_t*)(b + i * 1024) = regs[i];
-  }
   template <class SK> DEV void issue_to(int kt, SK sk) {
     const long e0 = (long)kt * BK * ld;
     const auto rs = make_rsrc(p + e0, total() - (unsigned long)e0 * sizeof(T));
@@ -372,13 +283,6 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Con
     tw = TapWalk{};
   }
   DEV void issue(int kt, char* tile) { issue_to(kt, DmaSink{tile + wave_id() * NIW * 1024}); }
-  // register staging: chunk i of this lane -> regs[i]; commit(tile, regs) stores it to LDS
-  DEV void issue_regs(int kt, u32x4_t* regs) { issue_to(kt, RegSink{regs}); }
-  DEV void commit(char* tile, const u32x4_t* regs) const {
-    char* b = tile + wave_id() * NIW * 1024 + (threadIdx.x & 63) * 16;
-#pragma unroll
-    for (int i = 0; i < NIW; i++) *(u32x4_t*)(b + i * 1024) = regs[i];
-  }
   template <class SK> DEV void issue_to(int kt, SK sk) {
     const auto rs = make_rsrc(xb, nb);
     if (g.SC % BK) {                 // channels not a multiple of BK: per-lane tap (rare shapes)
@@ -409,6 +313,53 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Con
     const unsigned cb = (unsigned)(tw.c0 * sizeof(T));
 #pragma unroll
     for (int i = 0; i < NIW; i++) sk(i, rs, base[i] + cb);
+  }
+};
+
+// 3x3 / stride 1 / pad 1 conv forward A operand for the 256x256 ping-pong kernel (bf16, SC a power-of-two multiple
+// of BK): rows = output pixels (b, oy, ox) of H x W, k = tap*SC + c.  Per lane and chunk only the element offset of
+// the CENTRE pixel is kept, plus a 9-bit tap-validity mask (every chunk's mask in one register), so a K tile's
+// offset is pix + a uniform (tap, channel) step and ConvFwdA's per-lane walker state (which spills beside the
+// ping-pong body's 240 live registers) is gone.
+template <int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Conv3A {
+  static constexpr int ROWS = R;
+  static constexpr bool KCL = true, RELU = RELU_;
+  typedef KCGeom<bf16, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
+  static_assert(NIW <= 3, "the tap masks of at most 3 chunks share one register");
+  const bf16* x; int B, H, W, SC, M, lgc;   // lgc = log2(SC / BK)
+  const bf16* xb; unsigned long nb;        // image window of this block (rebased descriptor)
+  int pix[NIW]; unsigned mask;
+  HD unsigned long img_bytes() const { return (unsigned long)H * W * SC * 2; }
+  HD bool buf_ok() const { return img_window_bytes(R, H * W, B, img_bytes()) < BUF_MAX && (BK << lgc) == SC; }
+  DEV void setup(int t0, int tid) {
+    const int lane = tid & 63, wave = wave_id(), hw = H * W;
+    const int b0 = min(t0, M - 1) / hw, b1 = min(t0 + R - 1, M - 1) / hw;
+    xb = x + (long)b0 * hw * SC;
+    nb = (unsigned long)(b1 - b0 + 1) * img_bytes();
+    mask = 0;
+#pragma unroll
+    for (int i = 0; i < NIW; i++) {
+      const int m = t0 + G::row(wave, i, lane);
+      pix[i] = 0;
+      if (m < M) {
+        const int b = m / hw, r = m - b * hw, oy = r / W, ox = r - oy * W;
+        pix[i] = ((b - b0) * hw + r) * SC + G::kel(wave, i, lane);
+        unsigned mk = 0;
+#pragma unroll
+        for (int t = 0; t < 9; t++)
+          if ((unsigned)(oy + t / 3 - 1) < (unsigned)H && (unsigned)(ox + t % 3 - 1) < (unsigned)W) mk |= 1u << t;
+        mask |= mk << (10 * i);
+      }
+    }
+  }
+  DEV void issue(int kt, char* tile) { issue_to(kt, DmaSink{tile + wave_id() * NIW * 1024}); }
+  template <class SK> DEV void issue_to(int kt, SK sk) {
+    const auto rs = make_rsrc(xb, nb);
+    const int tap = kt >> lgc, c0 = (kt - (tap << lgc)) * BK;
+    const int ty = tap / 3, tx = tap - 3 * ty;
+    const int toff = ((ty - 1) * W + (tx - 1)) * SC + c0;
+#pragma unroll
+    for (int i = 0; i < NIW; i++) sk(i, rs, ((mask >> (10 * i + tap)) & 1u) ? (unsigned)(pix[i] + toff) * 2u : BUF_OOB);
   }
 };
 
@@ -446,13 +397,6 @@ template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradA {
     tw = TapWalk{};
   }
   DEV void issue(int kt, char* tile) { issue_to(kt, DmaSink{tile + wave_id() * NIW * 1024}); }
-  // register staging: chunk i of this lane -> regs[i]; commit(tile, regs) stores it to LDS
-  DEV void issue_regs(int kt, u32x4_t* regs) { issue_to(kt, RegSink{regs}); }
-  DEV void commit(char* tile, const u32x4_t* regs) const {
-    char* b = tile + wave_id() * NIW * 1024 + (threadIdx.x & 63) * 16;
-#pragma unroll
-    for (int i = 0; i < NIW; i++) *(u32x4_t*)(b + i * 1024) = regs[i];
-  }
   template <class SK> DEV void issue_to(int kt, SK sk) {
     const auto rs = make_rsrc(yb, nb);
     const int TW = g.ntw > 0 ? g.ntw : 1;
@@ -509,13 +453,6 @@ template <typename T, int R, int NW = GEMM_WAVES> struct ConvDgradB {
     tw = TapWalk{};
   }
   DEV void issue(int kt, char* tile) { issue_to(kt, DmaSink{tile + wave_id() * NIW * 1024}); }
-  // register staging: chunk i of this lane -> regs[i]; commit(tile, regs) stores it to LDS
-  DEV void issue_regs(int kt, u32x4_t* regs) { issue_to(kt, RegSink{regs}); }
-  DEV void commit(char* tile, const u32x4_t* regs) const {
-    char* b = tile + wave_id() * NIW * 1024 + (threadIdx.x & 63) * 16;
-#pragma unroll
-    for (int i = 0; i < NIW; i++) *(u32x4_t*)(b + i * 1024) = regs[i];
-  }
   template <class SK> DEV void issue_to(int kt, SK sk) {
     const auto rs = make_rsrc(w, bytes());
     const int TW = g.ntw > 0 ? g.ntw : 1;
@@ -574,13 +511,6 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Wgr
     nk = -1;
   }
   DEV void issue(int kt, char* tile) { issue_to(kt, DmaSink{tile + wave_id() * NIW * 1024}); }
-  // register staging: chunk i of this lane -> regs[i]; commit(tile, regs) stores it to LDS
-  DEV void issue_regs(int kt, u32x4_t* regs) { issue_to(kt, RegSink{regs}); }
-  DEV void commit(char* tile, const u32x4_t* regs) const {
-    char* b = tile + wave_id() * NIW * 1024 + (threadIdx.x & 63) * 16;
-#pragma unroll
-    for (int i = 0; i < NIW; i++) *(u32x4_t*)(b + i * 1024) = regs[i];
-  }
   template <class SK> DEV void issue_to(int kt, SK sk) {
     if (g.RW % BK == 0) {
       if (kt != nk) { int k = kt * BK; int hw = g.RH * g.RW; pb = k / hw; int r = k - pb * hw; poy = r / g.RW; pox = r - poy * g.RW; }
@@ -631,11 +561,7 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Wgr
 };
 
 DEV bf16x8 relu_frag(bf16x8 v) {
-  typedef unsigned u4 __attribute__((ext_vector_type(4)));
-  u4 w = __builtin_bit_cast(u4, v);
-#pragma unroll
-  for (int i = 0; i < 4; i++) { unsigned m = (w[i] >> 15) & 0x00010001u; w[i] &= ~(m * 0xFFFFu); }
-  return __builtin_bit_cast(bf16x8, w);
+  return __builtin_bit_cast(bf16x8, relu16<bf16>(__builtin_bit_cast(uint4, v)));
 }
 DEV float relu_frag(float v) { return fmaxf(v, 0.f); }
 
@@ -786,20 +712,16 @@ __global__ void __launch_bounds__(GEMM_THREADS) igemm_kernel(LA la, LB lb, EPI e
 
   const int nt = kt1 - kt0;
   constexpr int PD = NST - 1;                 // LDS-DMA prefetch distance (tiles in flight)
-  constexpr bool REGA = IsReg<LA>::v;         // A register staged (transforming loader, 2 stages only)
-  static_assert(!REGA || NST == 2, "register-staged A needs 2 stages");
-  u32x4_t areg[REGA ? 2 * LA::NIW : 1];
   if (nt > 0) {
     // prologue: tiles 0 .. PD-1
 #pragma unroll
     for (int q = 0; q < PD; q++)
       if (q < nt) {
-        if constexpr (REGA) la.issue_regs(kt0 + q, areg); else la.issue(kt0 + q, smem + q * S::STAGE);
+        la.issue(kt0 + q, smem + q * S::STAGE);
         lb.issue(kt0 + q, smem + q * S::STAGE + S::ABYTES);
       }
     if constexpr (PD == 2) { if (nt > 1) wait_vmcnt<NL>(); else wait_vmcnt<0>(); }
     else wait_vmcnt<0>();
-    if constexpr (REGA) { la.commit(smem, areg, kt0); wait_lgkm0(); }
     __builtin_amdgcn_s_barrier();
     read_frags(0, smem, 0);
     int cur = 0;
@@ -808,7 +730,7 @@ __global__ void __launch_bounds__(GEMM_THREADS) igemm_kernel(LA la, LB lb, EPI e
       if (pre) {
         int st = cur + PD; if (st >= NST) st -= NST;
         char* nx = smem + st * S::STAGE;
-        if constexpr (REGA) la.issue_regs(kt0 + t + PD, areg); else la.issue(kt0 + t + PD, nx);
+        la.issue(kt0 + t + PD, nx);
         lb.issue(kt0 + t + PD, nx + S::ABYTES);
       }
       const char* stg = smem + cur * S::STAGE;
@@ -822,7 +744,6 @@ __global__ void __launch_bounds__(GEMM_THREADS) igemm_kernel(LA la, LB lb, EPI e
           // tile t+1 landed (own DMAs): PD-1 newer tiles may stay in flight
           if constexpr (PD == 2) { if (pre) wait_vmcnt<NL>(); else wait_vmcnt<0>(); }
           else wait_vmcnt<0>();
-          if constexpr (REGA) la.commit(smem + nxt * S::STAGE, areg, kt0 + t + 1);   // stage nxt: read last in t-1
           wait_lgkm0();
           __builtin_amdgcn_s_barrier();
           read_frags(b ^ 1, smem + nxt * S::STAGE, 0);
@@ -959,7 +880,6 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
     for_segments(ct, LDT, BM, BN, m0, n0, M, N, tid, NT, [&](int m, int n, const float* a, int r, int) {
       float pv[8], v[8], o[8];
       const long orow = rm.map(m);
-      if (orow < 0) return;                 // spatial-tile row outside the image (RowMap mode 3)
       if (fixed_cols) {
 #pragma unroll
         for (int e = 0; e < 8; e++) { pv[e] = a[e] + b8[e]; v[e] = pv[e] * s8[e] + h8[e]; }
@@ -1024,21 +944,24 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
       }
     });
     if (stats) {
-      // column statistics of pre over this tile's valid rows: 256 threads -> (col, row-phase)
-      int nph = NT / BN;
-      int c = tid % BN, ph = tid / BN;
-      int n = n0 + c;
+      // column statistics of pre over this tile's valid rows: thread -> (col, row phase).  The fp64 atomics of
+      // every tile of the grid would all land on the same 2N words; they are spread over S3OD_NREP replicas
+      // ([NREP][2][N], chosen by tile and row phase), which s3od_bn_finalize folds and clears
+      const int nph = NT / BN;
+      const int c = tid % BN, ph = tid / BN;
+      const int n = n0 + c;
       if (n < N) {
         float s = 0.f, q = 0.f;
-        float bn_ = bias ? bias[n] : 0.f;
+        const float bn_ = bias ? bias[n] : 0.f;
         for (int r = ph; r < BM; r += nph) {
           if (m0 + r >= M) break;
-          if (rm.mode == 3 && rm.map(m0 + r) < 0) continue;     // tile rows outside the image
-          float v = ct[r * LDT + c] + bn_;
+          const float v = ct[r * LDT + c] + bn_;
           s += v; q += v * v;
         }
-        atomicAdd(stats + n, (double)s);
-        atomicAdd(stats + N + n, (double)q);
+        const int rep = (int)(((unsigned)(blockIdx.y * gridDim.x + blockIdx.x) * (unsigned)nph + ph + (m0 / BM)) % S3OD_NREP);
+        double* st = stats + (long)rep * 2 * N;
+        atomicAdd(st + n, (double)s);
+        atomicAdd(st + N + n, (double)q);
       }
     }
     if (csum) {
@@ -1248,187 +1171,6 @@ __global__ void __launch_bounds__(GEMM_THREADS, 1) igemm_pp_kernel(LA la0, LB lb
   }
 }
 constexpr int PP_LDS = 128 * (256 + 4) * 4;   // C chunk (133 KB) >= the two 64 KB K stages
-
-// ------------------------------------------------------------------ halo ping-pong 3x3 conv (bf16)
-// 3x3 / stride 1 / pad 1 NHWC conv, Cin % 64 == 0, Cout % 256 == 0, on the 256x256 ping-pong schedule above,
-// with the A operand (im2col) formed from an input HALO in LDS instead of being gathered per K tile:
-//   * tile = 8 x 32 output pixels (256 virtual rows, RowMap mode 3) x 256 output channels;
-//   * K order = (channel chunk c of 64, tap): step s = 9 c + tap.  Chunk c's (8+2) x (32+2) x 64 halo sits in
-//     one of two LDS images for its 9 steps; every tap reads its A fragments at shifted pixel positions
-//     (per-lane base + immediate: halo row px, 16-B slot = chunk ^ (px & 7), conflict-free for every tap);
-//   * chunk c+1's halo trickles in during steps 9c .. 9c+5 (one 1-KiB LDS-DMA piece per wave per step,
-//     issued BEHIND that step's B halves, so the phase-3 vmcnt that retires the B halves leaves it in
-//     flight and the next step's wait retires it; read from step 9c+9 on);
-//   * B (weights [Cout][9][Cin]) and its buffers as in igemm_pp_kernel, the K-tile index remapped to
-//     tap * Cin/64 + c.  WAR on a halo image: its chunk-(c-1) reads end in phase 1 of step 9c-1, the first
-//     piece of chunk c+1 lands from phase 0 of step 9c (>= 2 phases later, as for the B halves).
-constexpr int HPP_PPW = 6, HPP_HB = 8 * HPP_PPW * 1024;          // 340 px x 128 B = 42.5 KiB -> 48 pieces
-constexpr int HPP_LDS = 2 * HPP_HB + 2 * 2 * 128 * 128;          // 2 halos + 2 x two B half images = 160 KiB
-static_assert(HPP_LDS <= 160 * 1024 && PP_LDS <= HPP_LDS, "halo ping-pong LDS budget");
-
-template <bool RELU, class LB, class EPI>
-__global__ void __launch_bounds__(GEMM_THREADS, 1) conv3x3_hpp_kernel(const bf16* __restrict__ x, LB lb0, EPI epi, int H, int W,
-                                                                       int Cin, int tiles_x, int tiles_y, int flags) {
-  constexpr int BN = 256, HB = 128 * 128, LDT = BN + 4, HC = 34, PX = 340;
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
-  const int wr = wave >> 2, wc = wave & 3;
-  int m0, n0, tile;
-  {
-    const int nwg = gridDim.x * gridDim.y;
-    const int L = blockIdx.y * gridDim.x + blockIdx.x;
-    const int q = nwg >> 3, r = nwg & 7, xcd = L & 7, idx = L >> 3;
-    const int Wl = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-    tile = Wl / gridDim.x; m0 = tile * 256; n0 = (Wl % gridDim.x) * BN;
-  }
-  const int txi = tile % tiles_x, t2 = tile / tiles_x, tyi = t2 % tiles_y, bb = t2 / tiles_y;
-  const int nch = Cin >> 6, nt = 9 * nch;
-  epi.prepare(0);
-  LB lb1 = lb0;
-  lb0.setup(n0, tid); lb1.setup(n0 + 128, tid);
-  char* Bb = smem + 2 * HPP_HB;                    // B buffer of step s: Bb + (s & 1) * 2 HB
-  const bool stag = !(flags & 1);
-  // halo DMA: piece p = 6 wave + i covers bytes [1024 p, +1024) of a halo image.  Everything is recomputed per
-  // piece from an opaque (scalar) i: one piece per wave per step, and any per-i value kept live across the chunk
-  // loop spills (the ping-pong body owns ~240 registers), whose reload's vmcnt(0) would serialise the DMA
-  const long img = (long)H * W * Cin;
-  const auto rx = make_rsrc(x + bb * img, (unsigned long)img * 2);
-  const int ty0 = tyi * 8 - 1, tx0 = txi * 32 - 1;
-  auto halo_piece = [&](int c, int i0, char* himg) {
-    int i = i0;
-    asm volatile("" : "+s"(i));
-    const int b = (wave * HPP_PPW + i) * 1024 + lane * 16, px = b >> 7, ch = ((b >> 4) & 7) ^ (px & 7);
-    const int hy = px / HC, gy = ty0 + hy, gx = tx0 + (px - hy * HC);
-    const bool ok = px < PX && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
-    blds16(rx, ok ? (unsigned)(((gy * W + gx) * Cin + c * 64) * 2 + ch * 16) : BUF_OOB, himg + (wave * HPP_PPW + i) * 1024);
-  };
-  // A fragment of block (qm, i), k-half kk, tap (dy, dx): halo px = Lw + off, Lw = 136 wr + (lane & 15),
-  // off = (2 qm + (i >> 1) + dy) * 34 + 16 (i & 1) + dx (compile-time).  Byte = 128 px + 16 (chunk ^ (px & 7)):
-  // the slot term of kk = 0 depends on the lane and on off & 7 only -> 8 per-lane bytes 16 (g ^ ((Lw + j) & 7))
-  // packed four to a register (ysl); kk = 1 reads chunk 4 + g = g ^ 4 -> the byte ^ 64
-  const int Lw = 4 * HC * wr + (lane & 15), yb0 = Lw * 128;
-  unsigned ysl[2] = {0u, 0u};
-  {
-    const int g = lane >> 4;
-#pragma unroll
-    for (int j = 0; j < 8; j++) ysl[j >> 2] |= (unsigned)(16 * (g ^ ((Lw + j) & 7))) << (8 * (j & 3));
-  }
-  PPFrag<LB::KCL> pfb; pfb.init(lane, wc & 1);
-  const int boff = LB::KCL ? (wc & 1) * 64 * 128 : 0;
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; i++)
-#pragma unroll
-    for (int j = 0; j < 4; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // one set of A fragments: the halo stays resident for the chunk, so quadrant row qm = 1 is read in phase 2
-  // (after qm = 0's last use) instead of beside qm = 0 as in igemm_pp_kernel (32 registers fewer)
-  bf16x8 fa[4][2], fb[2][2][2];
-  auto rdA = [&](const char* Hc, auto TAP, int qm) {
-    constexpr int tap = decltype(TAP)::value, dy = tap / 3, dx = tap % 3;
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-      for (int kk = 0; kk < 2; kk++) {
-        const int off = (2 * qm + (i >> 1) + dy) * HC + 16 * (i & 1) + dx;
-        const int j = off & 7, sl = (int)__builtin_amdgcn_ubfe(ysl[j >> 2], 8 * (j & 3), 8);
-        fa[i][kk] = *(const bf16x8*)(Hc + yb0 + (kk ? (sl ^ 64) : sl) + off * 128);
-      }
-  };
-  auto rdB = [&](const char* Bs, int qn) {
-#pragma unroll
-    for (int j = 0; j < 2; j++)
-#pragma unroll
-      for (int kk = 0; kk < 2; kk++) fb[qn][j][kk] = pfb.read(Bs, qn * 32 + j * 16, kk);
-  };
-  // sched_barrier(0) pins each phase's 16 MFMAs between its two barriers: with the 9 taps unrolled the scheduler
-  // would otherwise sink them below the next phase's LDS reads (destroying the compute / load alternation)
-  auto mm = [&](int qm, int qn) {
-    raw_barrier();
-    wait_lgkm0();
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; kk++)
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-#pragma unroll
-        for (int j = 0; j < 2; j++)
-          acc[qm * 4 + i][qn * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[qn][j][kk], fa[i][kk], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    raw_barrier();
-  };
-  auto kv = [&](int s) { return (s % 9) * nch + s / 9; };     // B K tile of step s
-  // RELU (the ReLU'd input of an RCU's first conv): applied once per halo in LDS instead of per fragment read;
-  // each wave rewrites the pieces it DMA'd itself, after its own vmcnt wait retired them
-  auto relu_own = [&](char* himg) {
-#pragma unroll 1
-    for (int i = 0; i < HPP_PPW; i++) {
-      bf16x8* q = (bf16x8*)(himg + (wave * HPP_PPW + i) * 1024 + lane * 16);
-      *q = relu_frag(*q);
-    }
-  };
-  // prologue: the whole halo of chunk 0, the B halves of step 0
-#pragma unroll
-  for (int i = 0; i < HPP_PPW; i++) halo_piece(0, i, smem);
-  lb0.issue(kv(0), Bb); lb1.issue(kv(0), Bb + HB);
-  wait_vmcnt<0>();
-  if constexpr (RELU) { relu_own(smem); wait_lgkm0(); }
-  raw_barrier();
-  if (wr && stag) raw_barrier();                   // stagger: the wr = 1 half runs one barrier behind
-  for (int c = 0; c < nch; c++) {
-    const char* Hc = smem + (c & 1) * HPP_HB;
-    char* Hn = smem + ((c + 1) & 1) * HPP_HB;
-    const bool nxt = c + 1 < nch;
-    auto step = [&](auto TAP) {
-      constexpr int tap = decltype(TAP)::value;
-      // keep the fragment addresses per step (otherwise all 9 x 16 are hoisted out of the chunk loop and spill)
-      asm volatile("" : "+v"(ysl[0]), "+v"(ysl[1]));
-#pragma unroll
-      for (int i = 0; i < LB::NIW; i++) { asm volatile("" : "+v"(lb0.vo[i])); asm volatile("" : "+v"(lb1.vo[i])); }
-      const int s = 9 * c + tap;
-      const char* Bs = Bb + (s & 1) * 2 * HB + (wc >> 1) * HB + boff;
-      char* Bn = Bb + ((s + 1) & 1) * 2 * HB;
-      const bool more = s + 1 < nt;
-      // phase 0: quadrant (0,0); B halves of step s+1, then (taps 0-5) one halo piece of chunk c+1
-      rdA(Hc, TAP, 0); rdB(Bs, 0);
-      if (more) { lb0.issue(kv(s + 1), Bn); lb1.issue(kv(s + 1), Bn + HB); }
-      if (tap < HPP_PPW && nxt) halo_piece(c + 1, tap, Hn);
-      if constexpr (RELU && tap == 7) { if (nxt) relu_own(Hn); }   // its pieces were retired in step 9c+6
-      mm(0, 0);
-      // phase 1: quadrant (0,1); the step's last B reads
-      rdB(Bs, 1);
-      mm(0, 1);
-      // phase 2: quadrant (1,1); A rows of quadrant row 1
-      rdA(Hc, TAP, 1);
-      mm(1, 1);
-      // phase 3: quadrant (1,0); retire the B halves of step s+1 (this step's halo piece stays in flight)
-      if (more) { if (tap < HPP_PPW && nxt) wait_vmcnt<1>(); else wait_vmcnt<0>(); }
-      mm(1, 0);
-    };
-    step(std::integral_constant<int, 0>{}); step(std::integral_constant<int, 1>{}); step(std::integral_constant<int, 2>{});
-    step(std::integral_constant<int, 3>{}); step(std::integral_constant<int, 4>{}); step(std::integral_constant<int, 5>{});
-    step(std::integral_constant<int, 6>{}); step(std::integral_constant<int, 7>{}); step(std::integral_constant<int, 8>{});
-  }
-  if (!wr && stag) raw_barrier();                  // re-align the two halves
-  float* ct = (float*)smem;
-#pragma unroll
-  for (int h = 0; h < 2; h++) {
-    lds_barrier();
-    if (wr == h) {
-#pragma unroll
-      for (int i = 0; i < 8; i++)
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const int r = i * 16 + (lane & 15), col = wc * 64 + j * 16 + (lane >> 4) * 4;
-          *(f32x4*)(ct + r * LDT + col) = acc[i][j];
-        }
-    }
-    lds_barrier();
-    epi(ct, LDT, m0 + h * 128, n0, tid, 128, BN, GEMM_THREADS);
-  }
-}
 
 // WM_: waves along M (0 = by tile shape); e.g. 512x64 tiles use WM_=8 for 64x64 per-wave tiles
 template <typename T, int BM, int BN, class LA, class LB, class EPI, int NST = 3, int WM_ = 0>

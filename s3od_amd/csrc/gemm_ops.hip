@@ -127,7 +127,7 @@ template <typename T> struct EpiQKV {
 template <typename T> struct EpiHeads {
   float* logits; T* hsave; const float* b1; const float* w2; const float* b2;
   int M, HW, NM;
-  RowMap rm;                                                  // staged row -> pixel (mode 0 dense, 3 tiles)
+  RowMap rm;                                                  // staged row -> pixel (mode 0 dense)
   DEV void prepare(int) {}
   DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN, int NT) const {
     const int C = 32 * NM, SPR = 4 * NM;                      // channels / 8-channel segments per row
@@ -172,155 +172,8 @@ template <typename T> struct EpiHeads {
   }
 };
 
-// ---------------------------------------------------------------- halo-tile 3x3 convolution
-// 3x3 / stride 1 / pad 1 NHWC bf16 conv with Cin = 64 for the full-resolution decoder maps, where
-// the implicit GEMM streams the whole [Cout][9*Cin] weight block from L2 for every 256-pixel tile
-// (288 B of weights per output pixel at Cout = 64) and re-stages a 9x-gathered A.  Here:
-//   * persistent workgroups (one per CU) keep ALL nine taps' weights resident in LDS;
-//   * one tile = 8 x 32 output pixels; its (8+2) x (32+2) x 64 input halo is written to LDS once
-//     and the nine taps read their A fragments at shifted positions; the NEXT tile's halo is
-//     prefetched into registers while the current tile computes (no barrier inside the tap loop);
-//   * 16-B chunks XOR-swizzled by (pixel & 7) / (cout & 7): conflict-free ds_read_b128 fragment
-//     reads for every tap offset (checked exhaustively against the gfx950 lane groups);
-//   * wave w computes output row w (32 pixels) x all Cout; the fp32 C tile is staged through the
-//     (consumed) halo region in row chunks and handed to the GEMM engine's block epilogues, with
-//     RowMap mode 3 mapping the tile-major virtual rows to pixels (rows outside the image skipped).
+// 8 x 32-pixel output tiles of the halo weight-gradient kernels below
 constexpr int HT_TH = 8, HT_TW = 32, HT_HR = HT_TH + 2, HT_HC = HT_TW + 2, HT_PX = HT_HR * HT_HC;
-template <int COUT> struct HaloShape {
-  static constexpr int CIN = 64, CPP = CIN / 8;           // 16-B chunks per pixel / weight row
-  static constexpr int WTS = 9 * COUT * 128;              // resident weights [tap][cout][64] bf16
-  static constexpr int HALO = HT_PX * 128;                // halo image [px][64] bf16
-  static constexpr int LDT = COUT + 4;
-  static constexpr int CR = (HALO / (LDT * 4)) >= 128 ? 128 : 64;   // C rows staged per chunk
-  static_assert(CR * LDT * 4 <= HALO, "C chunk must fit the halo region");
-  static constexpr int LDS = WTS + HALO;
-  static_assert(LDS <= 160 * 1024, "halo conv LDS budget");
-  static constexpr int HCH = HT_PX * CPP, HPT = (HCH + 511) / 512;
-};
-DEV int swz16(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
-
-template <int COUT, class EPI>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2)))
-conv3x3_halo_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EPI epi, int H, int W, int tiles_x, int tiles_y,
-                    int ntiles) {
-  typedef HaloShape<COUT> S;
-  constexpr int CPP = S::CPP;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* wts = smem;
-  char* halo = smem + S::WTS;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int lr = lane & 15, lg = lane >> 4;
-  // tiles of this workgroup: XCD x = blockIdx % 8 owns the contiguous tile range [x*n/8, (x+1)*n/8)
-  // (neighbouring tiles share halo rows in that XCD's L2); its workgroups stride through it
-  const int nwg = gridDim.x, xcd = blockIdx.x & 7, wpx = (nwg + 7 - xcd) >> 3, wi = blockIdx.x >> 3;
-  const int t_beg = (int)((long)ntiles * xcd / 8), t_end = (int)((long)ntiles * (xcd + 1) / 8);
-
-  // all nine taps' weights -> LDS, w: [COUT][9][64]
-  for (int c = tid; c < 9 * COUT * CPP; c += 512) {
-    const int ch = c % CPP, r = c / CPP, co = r % COUT, tap = r / COUT;
-    *(uint4*)(wts + swz16(tap * COUT + co, ch)) = *(const uint4*)(w + ((long)co * 9 + tap) * 64 + ch * 8);
-  }
-  uint4 hr[S::HPT];
-  auto prefetch = [&](int tile) {
-    const int txi = tile % tiles_x, t2 = tile / tiles_x, tyi = t2 % tiles_y, b = t2 / tiles_y;
-    const int ty0 = tyi * HT_TH - 1, tx0 = txi * HT_TW - 1;
-#pragma unroll
-    for (int i = 0; i < S::HPT; i++) {
-      const int c = tid + 512 * i;
-      hr[i] = make_uint4(0, 0, 0, 0);
-      if (c < S::HCH) {
-        const int px = c / CPP, ch = c - px * CPP, hy = px / HT_HC, hx = px - hy * HT_HC;
-        const int gy = ty0 + hy, gx = tx0 + hx;
-        if (gy >= 0 && gy < H && gx >= 0 && gx < W) hr[i] = *(const uint4*)(x + (((long)b * H + gy) * W + gx) * 64 + ch * 8);
-      }
-    }
-  };
-  int tile = t_beg + wi;
-  if (tile < t_end) prefetch(tile);
-  constexpr int NB = COUT / 16;
-  const int swb0 = (((0 + lg) ^ (lr & 7)) << 4), swb1 = (((4 + lg) ^ (lr & 7)) << 4);   // B chunk offsets (kk = 0, 1)
-  for (; tile < t_end; tile += wpx) {
-#pragma unroll
-    for (int i = 0; i < S::HPT; i++) {
-      const int c = tid + 512 * i;
-      if (c < S::HCH) { const int px = c / CPP, ch = c - px * CPP; *(uint4*)(halo + swz16(px, ch)) = hr[i]; }
-    }
-    lds_barrier();                                    // LDS only: a __syncthreads() would drain the stores
-    if (tile + wpx < t_end) prefetch(tile + wpx);     // next tile's halo in flight during the MFMAs
-    f32x4 acc[2][NB];
-#pragma unroll
-    for (int i = 0; i < 2; i++)
-#pragma unroll
-      for (int j = 0; j < NB; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 3
-    for (int tap = 0; tap < 9; tap++) {
-      const int dy = tap / 3, dx = tap - dy * 3;
-      const int p0 = (wave + dy) * HT_HC + dx + lr;   // this lane's halo pixel for pb = 0
-      const char* wt = wts + (tap * COUT + lr) * 128;
-#pragma unroll
-      for (int kk = 0; kk < 2; kk++) {
-        bf16x8 fa[2], fb[NB];
-#pragma unroll
-        for (int pb = 0; pb < 2; pb++) fa[pb] = *(const bf16x8*)(halo + swz16(p0 + pb * 16, kk * 4 + lg));
-#pragma unroll
-        for (int nb = 0; nb < NB; nb++) fb[nb] = *(const bf16x8*)(wt + nb * 16 * 128 + (kk ? swb1 : swb0));
-#pragma unroll
-        for (int pb = 0; pb < 2; pb++)
-#pragma unroll
-          for (int nb = 0; nb < NB; nb++) acc[pb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nb], fa[pb], acc[pb][nb], 0, 0, 0);
-      }
-    }
-    lds_barrier();                                    // halo consumed: its region now stages C
-    // lane owns C[px = pb*16 + lr][n = nb*16 + 4*lg .. +3] of output row `wave`
-    float* ct = (float*)halo;
-    const int vbase = tile * (HT_TH * HT_TW);
-    constexpr int WPC = S::CR / HT_TW;               // waves (output rows) per staged chunk
-#pragma unroll
-    for (int c0 = 0; c0 < HT_TH; c0 += WPC) {
-      if (wave >= c0 && wave < c0 + WPC) {
-        const int rr = (wave - c0) * HT_TW;
-#pragma unroll
-        for (int pb = 0; pb < 2; pb++)
-#pragma unroll
-          for (int nb = 0; nb < NB; nb++)
-            *(float4*)(ct + (rr + pb * 16 + lr) * S::LDT + nb * 16 + 4 * lg) =
-                make_float4(acc[pb][nb][0], acc[pb][nb][1], acc[pb][nb][2], acc[pb][nb][3]);
-      }
-      lds_barrier();
-      epi(ct, S::LDT, vbase + c0 * HT_TW, 0, tid, S::CR, COUT, 512);
-      lds_barrier();
-    }
-  }
-}
-
-static RowMap halo_rowmap(int H, int W) {
-  RowMap r{}; r.mode = 3; r.s = HT_TH; r.py = HT_TW; r.RH = cdiv(H, HT_TH); r.RW = cdiv(W, HT_TW); r.OH = H; r.OW = W;
-  return r;
-}
-// built: Cin 64 -> Cout 64 (conv fwd, stride-1 dgrad with the transposed weight) and 64 -> 96 (mask heads).
-// Default (S3OD_CONV_HALO=1): the mask heads only.  In the training step the 64 -> 64 fwd / dgrad ran
-// 2 % / 3 % SLOWER than the implicit GEMM (r02k): with the weights resident, one workgroup fills a CU,
-// so the epilogue's dependent global loads (ReLU' mask, residual) are not hidden behind another
-// workgroup's MFMAs.  S3OD_CONV_HALO=2 enables them too (dev), 0 disables the path.
-static bool halo_ok(int dtype, int C_in, int C_out) {
-  static const int knob = dev_knob("S3OD_CONV_HALO", 1);
-  return dtype == S3OD_BF16 && C_in == 64 && ((C_out == 96 && knob >= 1) || (C_out == 64 && knob >= 2));
-}
-template <int COUT, class EPI>
-static int launch_halo(const bf16* x, const bf16* w, EPI epi, int B, int H, int W, hipStream_t st) {
-  typedef HaloShape<COUT> S;
-  auto kfn = conv3x3_halo_kernel<COUT, EPI>;
-  static bool attr = false;
-  if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS); attr = true; }
-  const int tx = cdiv(W, HT_TW), ty = cdiv(H, HT_TH);
-  const long tiles = (long)B * tx * ty;
-  if (tiles * HT_TH * HT_TW >= (1L << 31)) { s3od_set_error("halo conv: too many pixels"); return 22; }
-  static int ncu = 0;
-  if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
-  const int nwg = (int)std::min<long>(std::max<long>(tiles, 8), (long)ncu);   // one persistent WG per CU, >= 8 so every XCD owns its range
-  hipLaunchKernelGGL(kfn, dim3(nwg), dim3(512), S::LDS, st, x, w, epi, H, W, tx, ty, (int)tiles);
-  return s3od_check_launch("conv3x3_halo");
-}
 
 // ---------------------------------------------------------------- register-weight 3x3 conv, 64 -> 64
 // The full-resolution 64-channel convs (upsample_2x.2 forward and its stride-1 data gradient) move
@@ -948,38 +801,6 @@ static int launch_convt_rw(const bf16* x, const bf16* wt, const float* bias, boo
   return s3od_check_launch("convT4s2_rw");
 }
 
-// ---------------------------------------------------------------- halo ping-pong 3x3 conv launcher
-// For 3x3 s1 bf16 convs with Cin % 64 == 0, Cout % 256 == 0 and at least two rounds of 256 tiles (the RCU /
-// layer_rn convs at 256^2 .. 128^2 maps).  OFF by default: measured slower than the 128x128 implicit GEMM
-// (tools/conv256_bench.py, bs 16, relu_in + bias + BN sums: 256^2 2.06 vs 1.72 ms, 128^2 0.55 vs 0.46 ms):
-// the 160 KiB of LDS (two halos + two B stages) leaves the B halves and the trickled halo pieces only one step
-// of latency cover, and in-order vmcnt makes every step's B wait also wait for the previous step's HBM halo
-// piece.  S3OD_CONV_HPP=1 enables it (auto), =2 forces it on any map (read per call: A/B and tests).
-static bool hpp_ok(int dtype, int B, int H, int W, int Cin, int Cout) {
-  const char* e = getenv("S3OD_CONV_HPP");
-  const int knob = e ? atoi(e) : 0;               // 0 off (default), 1 auto, 2 forced (tests: small maps)
-  if (knob == 0) return false;
-  const long tiles = (long)B * cdiv(H, HT_TH) * cdiv(W, HT_TW) * (Cout / 256);
-  return dtype == S3OD_BF16 && Cin % 64 == 0 && Cout % 256 == 0 && (tiles >= 512 || knob == 2) &&
-         (unsigned long)H * W * Cin * 2 < BUF_MAX && (long)H * W * Cin < (1L << 30);
-}
-template <class EPI>
-static int launch_hpp(const bf16* x, const bf16* wp, int relu_in, EPI e, int B, int H, int W, int Cin, int Cout, hipStream_t st) {
-  const int K = 9 * Cin, tx = cdiv(W, HT_TW), ty = cdiv(H, HT_TH);
-  DenseKC<bf16, 128> lb{wp, (long)K, Cout, K, 0};
-  if (!lb.buf_ok()) { s3od_set_error("conv hpp: weight window too large"); return 22; }
-  static const int flags = dev_knob("S3OD_PP_FLAGS", 0);
-  dim3 grid(Cout / 256, B * tx * ty);
-  auto go = [&](auto kfn) {
-    static bool attr = false;
-    if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, HPP_LDS); attr = true; }
-    hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), HPP_LDS, st, x, lb, e, H, W, Cin, tx, ty, flags);
-  };
-  if (relu_in) go(conv3x3_hpp_kernel<true, decltype(lb), EPI>);
-  else go(conv3x3_hpp_kernel<false, decltype(lb), EPI>);
-  return s3od_check_launch("conv3x3_hpp");
-}
-
 // ---------------------------------------------------------------- halo-tile 3x3 weight gradient
 // dW[co][tap][ci] = sum_px dy[px][co] * x[px + tap][ci] for a 3x3 / stride 1 / pad 1 conv with Cin = 64
 // and Cout = 64 / 96 (the full-resolution decoder convs).  The implicit-GEMM wgrad tiles N = 9*64 into
@@ -1516,6 +1337,19 @@ int s3od_qkv_rope_fwd(int dtype, int B, int Ntok, int P, int H, const void* x, c
   return 0;
 }
 
+// the 3x3 s1 p1 convs whose output channels fill 256-wide tiles and whose pixel tiles fill whole rounds of the
+// chip run on the ping-pong kernel (S3OD_CONV_PP=0, read per call, keeps the 128x128 implicit GEMM: A/B runs)
+// chip run on the ping-pong kernel when there are >= 8 rounds of tiles or K >= 9 * 512 (measured, tools/conv_cfg_bench.py,
+// bs 16: 256^2 RCU 1.38 vs 1.51-1.66 ms with BN sums, plain 1.21 vs 1.34-1.38 ms; 128^2 512 -> 256 0.56 vs 0.69-0.81 ms;
+// the 128^2 256 -> 256 RCU 0.39 vs 0.37-0.38 ms stays on 128x128 tiles)
+static bool conv_pp_ok(const ConvGeo& g, int M, int N) {
+  const int nch = g.SC / 64;
+  const long tiles = (long)(M / 256) * (N / 256);
+  return tl_cfg < 0 && gemm_cfg() < 0 && g.KH == 3 && g.KW == 3 && g.s == 1 && g.p == 1 && g.RH == g.SH && g.RW == g.SW &&
+         g.SC % 64 == 0 && (nch & (nch - 1)) == 0 && N % 256 == 0 && pp_pays(M, N) && (tiles >= 2048 || g.SC >= 512) &&
+         !getenv_zero("S3OD_CONV_PP");
+}
+
 // implicit-GEMM conv forward (im2col gathered per K tile by ConvFwdA); also the stride-1 3x3 data gradient run as a
 // forward conv of dy with the transposed, tap-reversed weight (s3od_conv_dgrad with wT)
 static int conv_fwd_igemm(int dtype, ConvGeo g, int M, int N, int K, int Cin, int Cout, const void* x, int relu_in,
@@ -1524,6 +1358,22 @@ static int conv_fwd_igemm(int dtype, ConvGeo g, int M, int N, int K, int Cin, in
                           hipStream_t st) {
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(K, KT<T>::BK);
+    if constexpr (sizeof(T) == 2) {
+      if (conv_pp_ok(g, M, N)) {
+        // 3x3 s1 p1 with 256-multiple output channels: the 256x256 ping-pong kernel (one workgroup per CU covers
+        // all 256 output channels of 256 pixels, so each im2col A tile is gathered once) with the Conv3A loader
+        auto pp = [&](auto rl) -> int {
+          Conv3A<128, decltype(rl)::value> la{};
+          la.x = (const bf16*)x; la.B = g.B; la.H = g.SH; la.W = g.SW; la.SC = g.SC; la.M = M;
+          la.lgc = __builtin_ctz((unsigned)(g.SC / 64));
+          DenseKC<bf16, 128> lb{(const bf16*)wp, (long)K, N, K, 0};
+          EpiStd<bf16, bf16> e{(bf16*)out, (long)Cout, 0, bias, scale, shift, (const bf16*)res1, (long)Cout, (const bf16*)res2,
+                               (long)Cout, (bf16*)pre, (long)Cout, stats, act, M, N, dense_rm(), colsum};
+          return launch_igemm<bf16, 256, 256, decltype(la), decltype(lb), decltype(e)>(la, lb, e, M, N, KTILES, 1, 1, st);
+        };
+        return relu_in ? pp(std::true_type{}) : pp(std::false_type{});
+      }
+    }
     auto go = [&](auto bn, auto rl) -> int {
       return with_cfg<T>(Cout <= 64 ? 3 : 1, [&](auto C0) -> int {
         typedef ConvCfg<decltype(C0), decltype(bn)::value> CC;
@@ -1550,27 +1400,11 @@ static int conv_fwd_igemm(int dtype, ConvGeo g, int M, int N, int K, int Cin, in
   return 0;
 }
 
-// LayerNorm fused into the QKV+RoPE projection's A operand (bf16; measurement prototype for north_star's
-// "fused LayerNorm+QKV projection", not used by the engine): x: [B*Ntok][D] fp32 residual stream, mean / rstd:
-// [B*Ntok] (s3od_layernorm_fwd with y = nullptr), ln_w / ln_b: [D]; outputs as s3od_qkv_rope_fwd.  128x128 tiles
-// (the register-staged A cannot use the ping-pong kernel's LDS-DMA schedule).
-int s3od_ln_qkv_rope_fwd(int dtype, int B, int Ntok, int P, int H, const float* x, const float* mean, const float* rstd,
-                         const float* ln_w, const float* ln_b, const void* w, const float* bias, const float* cos_t,
-                         const float* sin_t, void* q, void* k, void* v, void* stream) {
-  S3OD_REQUIRE(dtype == S3OD_BF16, "ln_qkv_rope_fwd: bf16 only");
-  const int D = 64 * H, N = 3 * D, M = B * Ntok;
-  LnA<128> la{x, (long)D, M, D, mean, rstd, ln_w, ln_b};
-  DenseKC<bf16, 128> lb{(const bf16*)w, (long)D, N, D, 0};
-  EpiQKV<bf16> e{(bf16*)q, (bf16*)k, (bf16*)v, bias, cos_t, sin_t, M, Ntok, P, H};
-  S3OD_REQUIRE(la.buf_ok(), "ln_qkv_rope_fwd: operand window too large");
-  return launch_igemm<bf16, 128, 128, decltype(la), decltype(lb), decltype(e), 2>(la, lb, e, M, N, cdiv(D, 64), 1, 1,
-                                                                                   (hipStream_t)stream);
-}
-
 // ---------------------------------------------------------------------------------- convs
 // NHWC activations, weights repacked [Cout][KH][KW][Cin].
 // pre = conv(relu?(x)) + bias[n]; out[b,oy,ox,n] = act(pre*scale[n] + shift[n]) (+res1 +res2);
-// stats: BN batch sums of pre.
+// stats: BN batch sums of pre, fp64 [S3OD_NREP = 32][sum | sum of squares][Cout] replicas, all zero on entry
+// (s3od_bn_finalize folds and clears them).
 int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW,
                   int stride, int pad, const void* x, int relu_in, const void* wp,
                   const float* bias, const float* scale, const float* shift, int act, const void* res1, const void* res2,
@@ -1587,20 +1421,6 @@ int s3od_conv_fwd(int dtype, int B, int H, int W, int Cin, int OH, int OW, int C
       !scale && !shift && !res1 && !res2 && !pre && !colsum && (act == ACT_NONE || act == ACT_RELU) && rw_ok(dtype, B, H, W))
     return act == ACT_RELU ? launch_rw<2, 64>((const bf16*)x, (const bf16*)wp, bias, nullptr, nullptr, (bf16*)out, B, H, W, st)
                            : launch_rw<0, 64>((const bf16*)x, (const bf16*)wp, bias, nullptr, nullptr, (bf16*)out, B, H, W, st);
-  if (KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && hpp_ok(dtype, B, H, W, Cin, Cout)) {
-    RowMap rm = halo_rowmap(H, W);
-    const int Mv = B * rm.RH * rm.RW * HT_TH * HT_TW;
-    EpiStd<bf16, bf16> e{(bf16*)out, (long)Cout, 0, bias, scale, shift, (const bf16*)res1, (long)Cout, (const bf16*)res2, (long)Cout,
-                         (bf16*)pre, (long)Cout, stats, act, Mv, N, rm, colsum};
-    return launch_hpp((const bf16*)x, (const bf16*)wp, relu_in, e, B, H, W, Cin, Cout, st);
-  }
-  if (KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && !relu_in && !stats && Cout == 64 && halo_ok(dtype, Cin, Cout)) {
-    RowMap rm = halo_rowmap(H, W);
-    const int Mv = B * rm.RH * rm.RW * HT_TH * HT_TW;
-    EpiStd<bf16, bf16> e{(bf16*)out, (long)Cout, 0, bias, scale, shift, (const bf16*)res1, (long)Cout, (const bf16*)res2, (long)Cout,
-                         (bf16*)pre, (long)Cout, nullptr, act, Mv, N, rm, colsum};
-    return launch_halo<64>((const bf16*)x, (const bf16*)wp, e, B, H, W, st);
-  }
   return conv_fwd_igemm(dtype, g, M, N, K, Cin, Cout, x, relu_in, wp, bias, scale, shift, act, res1, res2, out, pre, stats,
                         colsum, st);
 }
@@ -1632,16 +1452,6 @@ int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
     ConvGeo gf{}; gf.B = B; gf.SH = H; gf.SW = W; gf.SC = Cout; gf.RH = H; gf.RW = W; gf.KH = 3; gf.KW = 3; gf.s = 1; gf.p = 1;
     return conv_fwd_igemm(dtype, gf, B * H * W, Cin, 9 * Cout, Cout, Cin, dy, 0, wT, bias, scale, shift, act, res1, res2, dx,
                           nullptr, nullptr, colsum, (hipStream_t)stream);
-  }
-  if (wT && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && !stats && Cin == 64 && Cout == 64 &&
-      halo_ok(dtype, Cout, Cin)) {
-    // stride-1 3x3 data gradient = forward conv of dy with the transposed, tap-reversed weight wT
-    // ([Cin][3][3][Cout], packed by s3od_repack_multi mode 1) on the halo-tile kernel
-    RowMap rm = halo_rowmap(H, W);
-    const int Mv = B * rm.RH * rm.RW * HT_TH * HT_TW;
-    EpiStd<bf16, bf16> e{(bf16*)dx, (long)Cin, 0, bias, scale, shift, (const bf16*)res1, (long)Cin, (const bf16*)res2, (long)Cin,
-                         (bf16*)pre, (long)Cin, nullptr, act, Mv, Cin, rm, colsum};
-    return launch_halo<64>((const bf16*)dy, (const bf16*)wT, e, B, H, W, (hipStream_t)stream);
   }
   ConvGeo g0{}; g0.B = B; g0.SH = OH; g0.SW = OW; g0.SC = Cout; g0.KH = KH; g0.KW = KW; g0.s = stride; g0.p = pad;
   hipStream_t st = (hipStream_t)stream;
@@ -1748,11 +1558,6 @@ int s3od_mask_heads_fwd(int dtype, int B, int H, int W, int NM, const void* feat
   hipStream_t st = (hipStream_t)stream;
   if (N == 96 && rw_ok(dtype, B, H, W) && (long)3 * H * W * 4 < (1L << 31))
     return launch_rw<3, 64>((const bf16*)feat, (const bf16*)w1p, b1, nullptr, nullptr, (bf16*)hsave, B, H, W, st, w2, b2, logits);
-  if (N == 96 && halo_ok(dtype, 64, N)) {
-    RowMap rm = halo_rowmap(H, W);
-    EpiHeads<bf16> e{logits, (bf16*)hsave, b1, w2, b2, B * rm.RH * rm.RW * HT_TH * HT_TW, H * W, NM, rm};
-    return launch_halo<96>((const bf16*)feat, (const bf16*)w1p, e, B, H, W, st);
-  }
   DISPATCH_T(dtype, {
     constexpr int BM = 128;
     ConvFwdA<T, BM> la{}; la.x = (const T*)feat; la.g = g; la.M = M; la.relu = 0;

@@ -19,7 +19,7 @@ on the GPU with one fused HIP launch per sample (``s3od_augment_sample``, data_o
 * mode "synthetic" (transforms.py:65-220): the "regular" geometry + the synthetic groups, each a
   OneOf with the reference's probabilities and member weights: colour (ColorJitter 0.4/0.4/0.3/0.2 |
   HueSaturationValue 25/35/30 | CLAHE 4.0 / 8x8 tiles), noise (ISONoise | GaussNoise 0.25-0.6 |
-  MultiplicativeNoise), quality (ImageCompression 50-95: 8x8 DCT, 4:2:0 chroma, libjpeg tables |
+  MultiplicativeNoise), quality (ImageCompression 30-80: 8x8 DCT, 4:2:0 chroma, libjpeg tables |
   Downscale 0.4-0.7), lighting (RandomShadow 1-3 pentagons | RandomBrightnessContrast 0.4/0.4), blur
   (MotionBlur | GaussianBlur 3-7 | Defocus 2-6 | ZoomBlur 1-1.1), colour space (ToSepia | ToGray |
   ChannelShuffle, p 0.05), distortion (OpticalDistortion 0.3 | GridDistortion 6 steps | ElasticTransform |
@@ -270,6 +270,10 @@ class GpuAugment:
 
     def __init__(self, image_size: int, mode: str = "regular", device=None, seed: Optional[int] = None):
         self.S, self.mode = int(image_size), mode
+        if mode == "synthetic" and self.S % 8:
+            # CLAHE's 8x8 tile grid (drawn for ~10 % of synthetic samples) is built for S % 8 == 0: fail here,
+            # not at a random step
+            raise ValueError(f"GpuAugment: synthetic mode needs image_size divisible by 8 (CLAHE tiles), got {self.S}")
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         # every data-parallel rank draws its own augmentation stream (the reference seeds each
         # worker from torch.initial_seed(), which differs per rank / worker)
@@ -337,8 +341,10 @@ class GpuAugment:
             elif n == 1:                                        # ISONoise defaults: color_shift 0.01-0.05, intensity 0.1-0.5
                 q = q or SynthParams.identity()
                 q.iso_color_shift, q.iso_intensity = r.uniform(0.01, 0.05), r.uniform(0.1, 0.5)
-            elif n == 2:                                        # MultiplicativeNoise(0.9-1.1), per_channel=False
-                mult = [r.uniform(0.9, 1.1)] * 3
+            elif n == 2:                                        # MultiplicativeNoise(0.9-1.1): one multiplier per channel
+                # (albumentations 2.0.8, pinned uv.lock:249-267, samples shape [num_channels] unless elementwise;
+                # its per_channel argument is deprecated.  Parity unpinned: albumentations is not installed here)
+                mult = [r.uniform(0.9, 1.1) for _ in range(3)]
             if q is not None:                                   # Sharpen / ISONoise: the two-stage regular chain
                 q.order = 1
                 q.bright, q.contrast, q.sat, q.hue = bright, contrast, sat, hue
@@ -427,8 +433,9 @@ class GpuAugment:
             q.iso_color_shift, q.iso_intensity = r.uniform(0.01, 0.03), r.uniform(0.08, 0.3)
         elif g == 1:
             q.gauss_std = r.uniform(0.25, 0.6)
-        elif g == 2:
-            q.mult[0] = q.mult[1] = q.mult[2] = r.uniform(0.9, 1.1)
+        elif g == 2:                                          # one multiplier per channel (as the regular mode)
+            for i in range(3):
+                q.mult[i] = r.uniform(0.9, 1.1)
         g = _one_of(r, 0.5, [0.4, 0.3])                       # ImageCompression | Downscale
         if g == 0:
             q.jpeg_quality = r.randint(30, 80)

@@ -13,7 +13,6 @@ Reference structure: src/s3od/model.py:62-467 and tf:models/dinov3_vit/modeling_
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass, field
 
 import torch
@@ -23,10 +22,9 @@ from .weights import OUT_CH, VARIANTS
 
 NREG = 4
 ACT_NONE, ACT_RELU, ACT_GELU, ACT_GELU_BWD, ACT_RELU_BWD = 0, 1, 2, 3, 4
-# bf16 training: the up-projection saves gelu'(v) (one erf for both outputs) and the down dgrad multiplies by it
-# (S3OD_GELU_SG=0: the pre-activation + GELU' form, for A/B runs)
+# bf16 training: the up-projection saves gelu'(v) (one erf for both outputs) and the down dgrad multiplies by it;
+# the f32 strict path keeps the pre-activation and the exact erf GELU' (ACT_GELU_BWD)
 ACT_GELU_SG, ACT_MUL = 5, 6
-_GELU_SG = os.environ.get("S3OD_GELU_SG", "1") != "0"
 
 
 def _E(ref, n, dt, dev):
@@ -285,7 +283,7 @@ class DPTEngine:
                       scale=P[p + "layer_scale1.lambda1"], res1=xs, res_f32=True, out_f32=True, pre=u1)
             L("s3od_layernorm_fwd", dt, xm, P[p + "norm2.weight"], P[p + "norm2.bias"], h2, mean2, rstd2, M, D, 1e-5, st)
             self._lin(h2, W8[f"up{i}"], M, MLP, D, a, bias=P[p + "mlp.up_proj.bias"],
-                      act=ACT_GELU_SG if (hpre is not None and dt == BF16 and _GELU_SG) else ACT_GELU, pre=hpre)
+                      act=ACT_GELU_SG if (hpre is not None and dt == BF16) else ACT_GELU, pre=hpre)
             xn = _E(None, (B, Nt, D), torch.float32, dev)
             self._lin(a, W8[f"down{i}"], M, D, MLP, xn, bias=P[p + "mlp.down_proj.bias"],
                       scale=P[p + "layer_scale2.lambda1"], res1=xm, res_f32=True, out_f32=True, pre=u2)
@@ -328,7 +326,7 @@ class DPTEngine:
         return out
 
     def _conv_bn_train(self, x, wt, B, h, w, bias, relu_in=False):
-        stats = self.zero_ws("bn_stats", 2 * 256, torch.float64, x.device)   # cleared by s3od_bn_finalize
+        stats = self.zero_ws("bn_stats", 32 * 2 * 256, torch.float64, x.device)   # S3OD_NREP replicas, cleared by s3od_bn_finalize
         z = self._conv(x, wt, B, h, w, 256, 256, 3, 1, 1, bias=bias, relu_in=relu_in, stats=stats)
         return dict(z=z, stats=stats)
 
@@ -416,8 +414,23 @@ class DPTEngine:
         return {"pred_masks": logits, "pred_iou": iou, "features": p1.permute(0, 3, 1, 2)}
 
     # ------------------------------------------------------------------ full forward
+    def _invalidate(self):
+        """After a failed call: the persistent zero workspaces may hold partial sums of kernels whose
+        clearing reader never ran, and BN counter bumps may be queued for a forward that did not finish.
+        Drop both, so the next call allocates fresh zeros and bumps only its own counters."""
+        self._zpool = {}
+        self._nbt = []
+
     def forward(self, x, train=False, rope_rescale=None, ctx: Ctx | None = None):
         """x: [B,3,H,W] fp32 CUDA (normalised image).  Returns the reference output dict."""
+        self._nbt = []
+        try:
+            return self._forward(x, train, rope_rescale, ctx)
+        except BaseException:
+            self._invalidate()
+            raise
+
+    def _forward(self, x, train, rope_rescale, ctx):
         if x.dtype != torch.float32:
             x = x.float()
         Hh, Ww = x.shape[2], x.shape[3]
@@ -625,7 +638,7 @@ class DPTEngine:
             L("s3od_layerscale_bwd", dt, dx, s["u2"], P[p + "layer_scale2.lambda1"], du, G[p + "layer_scale2.lambda1"],
               G[p + "mlp.down_proj.bias"], red_ws, M, D, st)
             self._wgrad_lin(du, s["a"], D, MLP, M, G[p + "mlp.down_proj.weight"])
-            self._dgrad_lin(du, W8[f"down{i}"], M, MLP, D, dhp, act=ACT_MUL if (dt == BF16 and _GELU_SG) else ACT_GELU_BWD, aux=s["hpre"],
+            self._dgrad_lin(du, W8[f"down{i}"], M, MLP, D, dhp, act=ACT_MUL if dt == BF16 else ACT_GELU_BWD, aux=s["hpre"],
                             colsum=G[p + "mlp.up_proj.bias"])
             self._wgrad_lin(dhp, s["h2"], MLP, D, M, G[p + "mlp.up_proj.weight"])
             self._dgrad_lin(dhp, W8[f"up{i}"], M, D, MLP, dh)
@@ -665,7 +678,11 @@ class DPTEngine:
         """Accumulate parameter gradients into G (name -> fp32 tensor, reference layout; plus the
         fused views 'qkv_w{i}', 'heads1_w', 'heads1_b', 'heads2_w', 'heads2_b').  d_feat: optional
         gradient of the returned ``features`` (NCHW), added to path_1's."""
-        dtaps = self.decoder_backward(ctx, d_logits, d_iou, G, d_feat=d_feat)
-        if self.grad_hook is not None:
-            self.grad_hook("seg_head")
-        self.encoder_backward(ctx, dtaps, G)
+        try:
+            dtaps = self.decoder_backward(ctx, d_logits, d_iou, G, d_feat=d_feat)
+            if self.grad_hook is not None:
+                self.grad_hook("seg_head")
+            self.encoder_backward(ctx, dtaps, G)
+        except BaseException:
+            self._invalidate()
+            raise

@@ -89,6 +89,31 @@ def test_synthetic_params_host_logic():
         assert bytes(qa) == bytes(qb)
 
 
+def test_synthetic_mode_rejects_sizes_clahe_cannot_tile():
+    """CLAHE's 8x8 tile grid needs S % 8 == 0: the synthetic pipeline fails when built, not at the random
+    step that first draws CLAHE."""
+    import pytest
+    from s3od_amd.data import GpuAugment
+    with pytest.raises(ValueError, match="divisible by 8"):
+        GpuAugment(100, mode="synthetic", device="cpu", seed=1)
+    GpuAugment(100, mode="regular", device="cpu", seed=1)     # regular mode draws no CLAHE
+
+
+def test_multiplicative_noise_draws_one_multiplier_per_channel():
+    """albumentations 2.x MultiplicativeNoise samples shape [num_channels] (per_channel deprecated)."""
+    from s3od_amd.data import GpuAugment
+    aug = GpuAugment(64, mode="synthetic", device="cpu", seed=7)
+    img = np.zeros((64, 64, 3), np.uint8)
+    seen = 0
+    for _ in range(300):
+        q, _, _ = aug.synth_params(img)
+        m = list(q.mult)
+        if m != [1.0, 1.0, 1.0]:
+            assert len(set(m)) == 3 and all(0.9 <= v <= 1.1 for v in m)
+            seen += 1
+    assert seen > 0
+
+
 def test_grid_distortion_maps_cover_the_image():
     """GridDistortion(num_steps=6) normalised steps: the source maps start at 0, increase, and end at the
     image width (so the distorted grid never leaves the image), for sizes that are not multiples of 6."""

@@ -1,18 +1,18 @@
-"""GPU: the halo-tile 3x3 convolution (csrc/gemm_ops.hip conv3x3_halo_kernel) that serves the bf16
-full-resolution decoder convs — upsample_2x.2 (64->64 + ReLU), the mask heads (64->96, fused ReLU +
-1x1 + hsave) and the stride-1 data gradient 64<-64 with the ReLU' mask and the bias column sums
-(64<-96 stays on the implicit GEMM and is checked here too) — against fp32 PyTorch convolutions of the same bf16 operands (reference semantics:
-nn.Conv2d in src/s3od/model.py:437-467).  Ragged sizes exercise partial tiles at the right and
-bottom edges (RowMap mode 3 drops the rows outside the image).  Tolerance: bf16 output rounding
-(max-abs <= 2e-2 of the output scale)."""
+"""GPU: the bf16 full-resolution decoder convs -- upsample_2x.2 (64->64 + ReLU) and its stride-1 data gradient with
+the ReLU' mask and bias column sums (register-weight kernel conv3x3_c64_rw_kernel), the mask heads (64->96, fused
+ReLU + 1x1 + hsave), the 64<-96 data gradient, the halo-tile / LDS-DMA weight gradients, the ConvTranspose2d(128, 64,
+4, 2, 1) sub-pixel kernel and its strided data / weight gradients -- against fp32 PyTorch convolutions of the same
+bf16 operands (reference semantics: nn.Conv2d / ConvTranspose2d in src/s3od/model.py:437-467).  Ragged sizes exercise
+partial tiles at the right and bottom edges.  The specialised kernels' implicit-GEMM fall-backs (f32, very large maps)
+are checked too through the S3OD_CONVT_RW=0 / S3OD_WGRAD_DMA=0 test hooks (read per call).  Tolerance: bf16 output
+rounding (max-abs <= 2e-2 of the output scale)."""
+import os
+
 import pytest
 import torch
 import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
-# The 64 -> 64 fwd / dgrad halo paths are opt-in (S3OD_CONV_HALO=2, read once per process): under the
-# default these cases check the implicit-GEMM path against the same fp32 reference; run this file
-# alone with S3OD_CONV_HALO=2 to check the halo kernel on them (done when it was built: 6/6 passed).
 BF16 = 1
 ACT_RELU, ACT_RELU_BWD = 1, 4
 

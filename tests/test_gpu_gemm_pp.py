@@ -161,3 +161,65 @@ def test_pp_gelu_saved_derivative_pair(M, N, K):
     L("s3od_linear_dgrad", BF16, M, N, Kd, dy, Kd, wd, 6, gsave, N, dx, N, 0, 0, 0, 0, None, s)
     torch.cuda.synchronize()
     assert rel_l2(dx.float(), (dy.float() @ wd.float()) * ref_g) < 6e-3
+
+
+def test_pp_production_rows_65616():
+    """The bs-16 1024^2 step's own row count, M = 16 * 4101 = 65616 (256 full 256-row panels x N tiles on the
+    ping-pong kernel + an 80-row tail launch), for the ViT linears that select the ping-pong kernel there: QKV + RoPE
+    (N 2304, K 768), the up-projection with the saved-gelu' pair (N 3072, K 768), the down-projection forward with
+    LayerScale + fp32 residual (N 768, K 3072), the up-projection dgrad accumulated in place (N 768, K 3072) and the
+    up-projection wgrad (3072 x 768 over 65616 rows).  The MLP hidden tensors are 403 MB each."""
+    torch.manual_seed(65616)
+    L, s = _lib()
+    B, Nt, P, H = 16, 4101, 4096, 12
+    D, F = 64 * H, 4 * 64 * H
+    M = B * Nt
+    x = r(M, D)
+    # QKV + RoPE + head split
+    w, b = r(3 * D, D, scale=D ** -0.5), r(3 * D, dt=torch.float32)
+    ang = torch.rand(P, 32, device="cuda") * 6.28
+    cs = torch.cat([ang.cos(), ang.cos()], 1).contiguous()
+    sn = torch.cat([ang.sin(), ang.sin()], 1).contiguous()
+    q, k, v = (torch.empty(B * H, Nt, 64, device="cuda", dtype=torch.bfloat16) for _ in range(3))
+    L("s3od_qkv_rope_fwd", BF16, B, Nt, P, H, x, w, b, cs, sn, q, k, v, s)
+    y = (x.float() @ w.float().t() + b).view(B, Nt, 3, H, 64).permute(2, 0, 3, 1, 4).reshape(3, B * H, Nt, 64)
+    pt = y[:2, :, Nt - P:]
+    y[:2, :, Nt - P:] = pt * cs + torch.cat([-pt[..., 32:], pt[..., :32]], -1) * sn
+    torch.cuda.synchronize()
+    QSCALE = 0.125 * 1.4426950408889634
+    assert rel_l2(q.float(), y[0] * QSCALE) < 4e-3
+    assert rel_l2(k.float(), y[1]) < 4e-3 and rel_l2(v.float(), y[2]) < 4e-3
+    del y, pt, q, k, v
+    # up-projection: GELU(v) and gelu'(v)
+    wu, bu = r(F, D, scale=D ** -0.5), r(F, dt=torch.float32)
+    a = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
+    gs = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
+    L("s3od_linear_fwd", BF16, M, F, D, x, D, wu, bu, None, None, 5, None, F, None, 0, 0, a, F, 0, gs, F, 0, 0, 0, s)
+    pre = (x.float() @ wu.float().t() + bu)
+    ref = torch.nn.functional.gelu(pre)
+    torch.cuda.synchronize()
+    assert rel_l2(a.float(), ref) < 5e-3
+    pre.requires_grad_(True)
+    ref_g = torch.autograd.grad(torch.nn.functional.gelu(pre).sum(), pre)[0]
+    assert rel_l2(gs.float(), ref_g) < 5e-3
+    del pre, ref, ref_g, gs
+    # down-projection forward: (a wd^T + bd) * ls + residual (fp32)
+    wd, bd, ls = r(D, F, scale=F ** -0.5), r(D, dt=torch.float32), r(D, dt=torch.float32)
+    res = r(M, D, dt=torch.float32)
+    out = torch.empty(M, D, device="cuda")
+    L("s3od_linear_fwd", BF16, M, D, F, a, F, wd, bd, ls, None, 0, res, D, None, 0, 1, out, D, 1, None, D, 0, 0, 0, s)
+    torch.cuda.synchronize()
+    assert rel_l2(out, (a.float() @ wd.float().t() + bd) * ls + res) < 1e-5
+    # up-projection dgrad, accumulated in place into an fp32 gradient
+    dh = r(M, F)
+    dx0 = r(M, D, dt=torch.float32)
+    dx = dx0.clone()
+    L("s3od_linear_dgrad", BF16, M, D, F, dh, F, wu, 0, dx, D, dx, D, 1, 0, 0, 0, None, s)
+    torch.cuda.synchronize()
+    assert rel_l2(dx, dx0 + dh.float() @ wu.float()) < 1e-5
+    # up-projection wgrad over all 65616 rows
+    dw0 = r(F, D, dt=torch.float32)
+    dw = dw0.clone()
+    L("s3od_linear_wgrad", BF16, F, D, M, dh, F, x, D, dw, 0, s)
+    torch.cuda.synchronize()
+    assert rel_l2(dw, dw0 + dh.float().t() @ x.float()) < 1e-5
