@@ -560,6 +560,49 @@ template <typename T, int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Wgr
   }
 };
 
+// 3x3 / stride 1 / pad 1 weight-gradient B operand for the ping-pong kernel (bf16, MC image):
+// B[k = output pixel][n = tap*Cin + cin] = x[pixel shifted by the tap][cin].  With W % BK == 0 a K tile's 64 pixels
+// are one run of an image row and Cin % 256 == 0 puts a 256-column tile inside ONE tap, so the tile is a contiguous
+// 64-pixel run of x shifted by (dy, dx): per lane only its k-row and its channel offset are kept, the row / image
+// walk is uniform (scalar) and just the first / last pixel of a row can fall outside the image (dx = -1 / +1).
+template <int R, bool RELU_ = false, int NW = GEMM_WAVES> struct Wgrad3B {
+  static constexpr int ROWS = R;
+  static constexpr bool KCL = false, RELU = RELU_;
+  typedef MCGeom<bf16, R, NW> G; static constexpr int NIW = G::NIW, BK = G::BK;
+  const bf16* x; int B, H, W, Cin;
+  int tdy, tdx;                                  // this block's tap offsets (uniform)
+  int nk, pb, py, px0;                           // uniform walker: next K tile, its image / row / first column
+  int kr[NIW]; unsigned lo[NIW];
+  HD unsigned long img_bytes() const { return (unsigned long)H * W * Cin * 2; }
+  HD bool buf_ok() const { return img_bytes() < BUF_MAX && W % BK == 0 && Cin % 256 == 0; }
+  DEV void setup(int t0, int tid) {
+    const int lane = tid & 63, wave = wave_id();
+    const int tap = t0 / Cin, c0 = t0 - tap * Cin;
+    tdy = tap / 3 - 1; tdx = tap - 3 * (tap / 3) - 1;
+#pragma unroll
+    for (int i = 0; i < NIW; i++) {
+      kr[i] = G::krow(wave, i, lane);
+      lo[i] = (unsigned)((kr[i] * Cin + c0 + G::col(wave, i, lane)) * 2);
+    }
+    nk = -1;
+  }
+  DEV void issue(int kt, char* tile) { issue_to(kt, DmaSink{tile + wave_id() * NIW * 1024}); }
+  template <class SK> DEV void issue_to(int kt, SK sk) {
+    if (kt != nk) { const int p = kt * BK, hw = H * W; pb = p / hw; const int r = p - pb * hw; py = r / W; px0 = r - py * W; }
+    else { px0 += BK; if (px0 >= W) { px0 = 0; if (++py >= H) { py = 0; pb++; } } }
+    nk = kt + 1;
+    const int yy = py + tdy;
+    const bool rowok = pb < B && (unsigned)yy < (unsigned)H;
+    const auto rs = make_rsrc(x + (long)(rowok ? pb : 0) * H * W * Cin, img_bytes());
+    const int base = ((yy * W + px0 + tdx) * Cin) * 2;          // pixel (yy, px0 + dx), channel 0 (may be < 0)
+#pragma unroll
+    for (int i = 0; i < NIW; i++) {
+      const bool ok = rowok && (unsigned)(px0 + kr[i] + tdx) < (unsigned)W;
+      sk(i, rs, ok ? (unsigned)(base + (int)lo[i]) : BUF_OOB);
+    }
+  }
+};
+
 DEV bf16x8 relu_frag(bf16x8 v) {
   return __builtin_bit_cast(bf16x8, relu16<bf16>(__builtin_bit_cast(uint4, v)));
 }
@@ -1082,6 +1125,15 @@ __global__ void __launch_bounds__(GEMM_THREADS, 1) igemm_pp_kernel(LA la0, LB lb
   lb0.setup(n0, tid); lb1.setup(n0 + 128, tid);
   constexpr int NA = LA::NIW * 2;              // DMA instructions per wave for the two A halves
   const bool stag = !(flags & 1);              // dev knob S3OD_PP_FLAGS bit 0: no stagger
+  // CU desynchronisation (flags >> 8 = delay in units of 1024 cycles): every tile of a launch takes the same time, so
+  // the first round's workgroups reach their store-heavy epilogues together and every later round inherits that
+  // lock-step.  Delaying half of the first round (every other workgroup of each XCD) offsets the CUs' tile rounds so
+  // one half's epilogue stores run under the other half's main loop.
+  if (const int dl = flags >> 8) {
+    const int L = blockIdx.y * gridDim.x + blockIdx.x;
+    if (L < 256 && ((L >> 3) & 1))
+      for (int c = 0; c < dl; c++) __builtin_amdgcn_s_sleep(16);
+  }
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -1184,7 +1236,9 @@ static int launch_igemm(LA la, LB lb, EPI epi, int M, int N, int KTILES, int spl
     auto kfn = igemm_pp_kernel<LA, LB, EPI>;
     static bool attr = false;
     if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS); attr = true; }
-    static const int flags = dev_knob("S3OD_PP_FLAGS", 0);
+    static const int flags0 = dev_knob("S3OD_PP_FLAGS", 0);
+    const char* sd = getenv("S3OD_PP_STAGGER");      // per call: first-round delay (x 1024 cycles) for A/B runs
+    const int flags = flags0 | ((sd ? atoi(sd) : 0) << 8);
     dim3 grid(cdiv(N, BN), cdiv(M, BM), split * zdim_extra);
     hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), PP_LDS, st, la, lb, epi, KTILES, split, flags);
     return s3od_check_launch("igemm_pp");

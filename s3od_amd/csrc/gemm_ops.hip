@@ -1521,6 +1521,24 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
     hipLaunchKernelGGL(wgrad_permute_add_kernel, dim3(cdiv((long)M * N, 256)), dim3(256), 0, st, ws, dw, M, Cin, KH * KW);
     return s3od_check_launch("conv_wgrad permute");
   }
+  if (dtype == S3OD_BF16 && ws && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && W % 64 == 0 &&
+      Cin % 256 == 0 && Cout % 256 == 0 && tl_cfg < 0 && gemm_cfg() < 0 && !getenv_zero("S3OD_WGRAD_PP")) {
+    // the 256-channel RCU / layerK_rn weight gradients on the ping-pong kernel: one 256 x 256 tile = 256 output
+    // channels x one tap's 256 input channels, K = pixels split over ~one round of workgroups (fp32 atomics into the
+    // GEMM-layout workspace, then the permute into dW)
+    const int KTILES = NPIX / 64, tiles = (Cout / 256) * (N / 256);
+    int sp = split > 0 ? split : std::max(1, std::min(256 / tiles, KTILES / 8));
+    DenseMC<bf16, 128> la{(const bf16*)dy, (long)Cout, NPIX, Cout};
+    EpiWgrad e{ws, M, N, N, 1};
+    auto pp = [&](auto rl) -> int {
+      Wgrad3B<128, decltype(rl)::value> lb{}; lb.x = (const bf16*)x; lb.B = B; lb.H = H; lb.W = W; lb.Cin = Cin;
+      return launch_igemm<bf16, 256, 256, decltype(la), decltype(lb), decltype(e)>(la, lb, e, M, N, KTILES, sp, 1, st);
+    };
+    int rc = relu_x ? pp(std::true_type{}) : pp(std::false_type{});
+    if (rc) return rc;
+    hipLaunchKernelGGL(wgrad_permute_add_kernel, dim3(cdiv((long)M * N, 256)), dim3(256), 0, st, ws, dw, M, Cin, KH * KW);
+    return s3od_check_launch("conv_wgrad permute");
+  }
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(NPIX, KT<T>::BK);
     auto go = [&](auto bm, auto rl) -> int {

@@ -13,6 +13,7 @@ Reference structure: src/s3od/model.py:62-467 and tf:models/dinov3_vit/modeling_
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -616,7 +617,32 @@ class DPTEngine:
         dx[:, :1 + NREG].zero_()
         first_tap = True
         tap_of = {t: j for j, t in enumerate(self.taps)}
+        # weight gradients run on a side stream, concurrently with the data-gradient chain on the main stream: each
+        # wgrad only READS its two operands, so it may trail the chain; the chain waits for the reader's event before
+        # it overwrites an operand buffer one layer later (in practice long done).  Two single-pipeline kernels then
+        # share the CUs: one's store-bound epilogue / tail overlaps the other's MFMA main loop.
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream(dev) if os.environ.get("S3OD_BWD_SIDE", "1") != "0" else main   # (A/B: 0 = one stream)
+        ev_free = {}                                   # buffer -> event after its last side-stream reader
+
+        def on_side(fn, *bufs):
+            e = torch.cuda.Event()
+            e.record(main)
+            side.wait_event(e)
+            with torch.cuda.stream(side):
+                fn()
+            for b in bufs:
+                f = torch.cuda.Event()
+                f.record(side)
+                ev_free[b] = f
+
+        def claim(b):                                  # before the main stream overwrites buffer b
+            f = ev_free.pop(b, None)
+            if f is not None:
+                main.wait_event(f)
+
         du = _E(None, (M, D), T, dev)
+        du2 = _E(None, (M, D), T, dev)
         dhp = _E(None, (M, MLP), T, dev)
         dh = _E(None, (M, D), T, dev)
         dxm = _E(None, (B, Nt, D), torch.float32, dev)
@@ -635,32 +661,38 @@ class DPTEngine:
             p = f"encoder.model.layer.{i}."
             s = ctx.t[f"L{i}"]
             # ---- MLP half
+            claim("du")
             L("s3od_layerscale_bwd", dt, dx, s["u2"], P[p + "layer_scale2.lambda1"], du, G[p + "layer_scale2.lambda1"],
               G[p + "mlp.down_proj.bias"], red_ws, M, D, st)
-            self._wgrad_lin(du, s["a"], D, MLP, M, G[p + "mlp.down_proj.weight"])
+            on_side(lambda: self._wgrad_lin(du, s["a"], D, MLP, M, G[p + "mlp.down_proj.weight"]), "du")
+            claim("dhp")
             self._dgrad_lin(du, W8[f"down{i}"], M, MLP, D, dhp, act=ACT_MUL if dt == BF16 else ACT_GELU_BWD, aux=s["hpre"],
                             colsum=G[p + "mlp.up_proj.bias"])
-            self._wgrad_lin(dhp, s["h2"], MLP, D, M, G[p + "mlp.up_proj.weight"])
+            on_side(lambda: self._wgrad_lin(dhp, s["h2"], MLP, D, M, G[p + "mlp.up_proj.weight"]), "dhp")
             self._dgrad_lin(dhp, W8[f"up{i}"], M, D, MLP, dh)
             L("s3od_layernorm_bwd", dt, dh, s["xm"], s["mean2"], s["rstd2"], P[p + "norm2.weight"], dx, dxm,
               G[p + "norm2.weight"], G[p + "norm2.bias"], red_ws, M, D, st)
             # ---- attention half
-            L("s3od_layerscale_bwd", dt, dxm, s["u1"], P[p + "layer_scale1.lambda1"], du, G[p + "layer_scale1.lambda1"],
+            claim("du2")
+            L("s3od_layerscale_bwd", dt, dxm, s["u1"], P[p + "layer_scale1.lambda1"], du2, G[p + "layer_scale1.lambda1"],
               G[p + "attention.o_proj.bias"], red_ws, M, D, st)
-            self._wgrad_lin(du, s["o"], D, D, M, G[p + "attention.o_proj.weight"])
+            on_side(lambda: self._wgrad_lin(du2, s["o"], D, D, M, G[p + "attention.o_proj.weight"]), "du2")
             do = dh
-            self._dgrad_lin(du, W8[f"o{i}"], M, D, D, do)
+            self._dgrad_lin(du2, W8[f"o{i}"], M, D, D, do)
             # attention backward with the inverse RoPE / q scale / q,v bias sums fused into its stores
+            claim("dqkv")
             L("s3od_attn_bwd_qkv", dt, s["q"], s["k"], s["v"], s["o"], do, s["lse"], delta, ctx.t["cos"], ctx.t["sin"], NP,
               dqkv, G[p + "attention.q_proj.bias"], G[p + "attention.v_proj.bias"], qv_ws, B, H, Nt, st)
-            self._wgrad_lin(dqkv, s["h1"], 3 * D, D, M, G[f"qkv_w{i}"])
+            on_side(lambda: self._wgrad_lin(dqkv, s["h1"], 3 * D, D, M, G[f"qkv_w{i}"]), "dqkv")
             dh1 = dh
             self._dgrad_lin(dqkv, W8[f"qkv{i}"], M, D, 3 * D, dh1)
             L("s3od_layernorm_bwd", dt, dh1, s["x"], s["mean1"], s["rstd1"], P[p + "norm1.weight"], dxm, dxi,
               G[p + "norm1.weight"], G[p + "norm1.bias"], red_ws, M, D, st)
             dx, dxi = dxi, dx
             if self.grad_hook is not None:
-                self.grad_hook(f"layer{i}")
+                # the layer's gradients are final once both streams are past it: the hook (the DDP bucket all-reduce)
+                # is issued from the side stream after it has joined the main stream
+                on_side(lambda: self.grad_hook(f"layer{i}"))
         # ---- embeddings
         e = "encoder.embeddings."
         L("s3od_token_prefix_bwd", dx, G[e + "cls_token"], G[e + "register_tokens"], B, Nt, D, st)
@@ -668,11 +700,18 @@ class DPTEngine:
         L("s3od_cast_tap", dt, dx, dpatch, B, Nt, NP, D, st)
         self._colsum(dpatch, B * NP, D, G[e + "patch_embeddings.bias"])
         self._wgrad_lin(dpatch, ctx.t["cols"], D, 768, B * NP, G[e + "patch_embeddings.weight"])
+        main.wait_stream(side)                         # every weight gradient is final on the main stream
         lib().phase = None
         if self.grad_hook is not None:
             self.grad_hook("embeddings")
 
     grad_hook = None
+
+    def _side_stream(self, dev):
+        st = getattr(self, "_side", None)
+        if st is None or st.device != dev:
+            st = self._side = torch.cuda.Stream(device=dev)
+        return st
 
     def backward(self, ctx: Ctx, d_logits, d_iou, G, d_feat=None):
         """Accumulate parameter gradients into G (name -> fp32 tensor, reference layout; plus the

@@ -94,3 +94,34 @@ def test_conv_dgrad_as_forward_pp():
         _close(dx, _nhwc(ref))
         outs[knob] = dx
     _close(outs["1"], outs["0"], tol=1.6e-2)
+
+
+@pytest.mark.parametrize("B,H,W,Ci,relu", [(2, 37, 128, 256, 0), (3, 20, 64, 512, 1), (16, 64, 64, 256, 1)])
+def test_conv_wgrad_pp(B, H, W, Ci, relu):
+    """3x3 s1 weight gradient of a 256-output-channel conv on the ping-pong kernel (Wgrad3B loader: one tap's 256 input
+    channels per tile, pixels split over the grid, fp32 atomics into the GEMM-layout workspace, then the permute),
+    accumulated onto an existing gradient, vs torch's conv2d_weight of the same bf16 operands (ReLU'd input when
+    relu = 1: an RCU conv1); and vs the 128x128 implicit GEMM (S3OD_WGRAD_PP=0).  Odd H, several images per split."""
+    from s3od_amd._lib import lib, stream
+    Co = 256
+    g = torch.Generator(device="cuda").manual_seed(B * H + Ci)
+    dy = torch.randn(B, Co, H, W, device="cuda", generator=g).bfloat16()
+    x = torch.randn(B, Ci, H, W, device="cuda", generator=g).bfloat16()
+    xin = x.float().clamp_min(0) if relu else x.float()
+    dw0 = torch.randn(Co, Ci, 3, 3, device="cuda", generator=g)
+    ref = dw0 + torch.nn.grad.conv2d_weight(xin, (Co, Ci, 3, 3), dy.float(), padding=1)
+    ws = torch.zeros(Co * 9 * Ci, device="cuda")
+    outs = {}
+    for knob in ("1", "0"):
+        dw = dw0.clone()
+        os.environ["S3OD_WGRAD_PP"] = knob
+        try:
+            lib()("s3od_conv_wgrad", BF16, B, H, W, Ci, H, W, Co, 3, 3, 1, 1, _nhwc(dy), _nhwc(x), relu, dw, ws, 0, stream())
+        finally:
+            os.environ.pop("S3OD_WGRAD_PP", None)
+        torch.cuda.synchronize()
+        err = float((dw - ref).norm() / (ref - dw0).norm())
+        assert err < 1e-5, (knob, err)
+        outs[knob] = dw
+    assert float(ws.abs().max()) == 0.0          # the workspace is left all zero
+    assert float((outs["1"] - outs["0"]).norm() / (ref - dw0).norm()) < 1e-5

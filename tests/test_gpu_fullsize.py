@@ -142,22 +142,24 @@ def _grad_report(grads, sd):
     return worst_n, worst_c
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(900)
 def test_c3_multi_image_train_step_vs_oracle_1024():
-    """A MULTI-image production-size train step (bs 4, 1024^2: the bs-16 step's code path -- the > 4 GiB MLP window
-    handling aside -- with multi-image BN batch statistics, the M = 4 * 4101 GEMM tails, split-K wgrads over four
-    images) against the ORACLE's autograd (lightning_module.py:242-244; train-mode BN src/s3od/model.py:334-345),
-    not against the build's own f32 path: f32 strict at the bs-1 thresholds (loss 1e-4, logits 2e-4 max-rel on every
-    image, per-parameter grad norm 2e-3, cosine 0.999, BN running stats 1e-4), then bf16 (loss 2 %, per-parameter
-    cosine >= 0.99)."""
+    """A MULTI-image production-size train step (bs 2 at 1024^2: multi-image BN batch statistics, the M = 2 * 4101
+    GEMM tails, split-K wgrads over both images) against the ORACLE's autograd (lightning_module.py:242-244; train-mode
+    BN src/s3od/model.py:334-345), not against the build's own f32 path: f32 strict at the bs-1 thresholds (loss 1e-4,
+    logits 2e-4 max-rel on every image, per-parameter grad norm 2e-3, cosine 0.999, BN running stats 1e-4), then the
+    bf16 fast path (loss 2 %, per-parameter cosine >= 0.99).  bs 2, not 4: the fp32 oracle and the f32-strict engine
+    (fp32 MFMA, 1/16 of the bf16 rate) take ~1 min per image each, and the GPU box kills a test that is silent for
+    3 min; progress is printed per phase (visible with -s)."""
     from oracle import s3od_oracle as O
     from s3od_amd.model import DPTSegmentation
-    B = 4
+    B = 2
     x, masks = _batch(B, 1024, 33)
     sd = _oracle_sd(requires_grad=True)
     ref = O.forward(x, sd, train=True, rope_rescale=1.3)
     rloss, *_ = O.multi_mask_loss(ref, masks, 0)
     rloss.backward()
+    print(f"C3 bs{B}: oracle step done", flush=True)
     rpm = ref["pred_masks"].detach()
     del ref
     torch.cuda.empty_cache()

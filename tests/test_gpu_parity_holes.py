@@ -230,3 +230,39 @@ def test_features_gradient_vs_oracle():
         worst_n = max(worst_n, (en, n)); worst_c = min(worst_c, (c, n))
     assert worst_n[0] <= 2e-3, worst_n
     assert worst_c[0] >= 0.999, worst_c
+
+
+def test_failed_call_drops_zero_workspaces():
+    """a call that fails between an accumulating kernel and its clearing reader (here: the BN finalize of
+    the 3rd train-mode BN raises after its conv has added batch sums into the persistent workspace) must not leak
+    those partials or the queued num_batches_tracked bumps into later calls.  The engine drops both; the next
+    train-mode forward then equals a fresh model's, buffers included."""
+    from s3od_amd.model import DPTSegmentation
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(2, 3, 128, 128, generator=g).cuda()
+    m = DPTSegmentation(compute_dtype="bf16").cuda().train()
+    m._rope_rescale = 1.1
+    eng = m.engine()
+    orig, calls = eng._bn_train, {"n": 0}
+
+    def boom(*a, **k):
+        calls["n"] += 1
+        if calls["n"] == 3:
+            raise RuntimeError("injected failure")
+        return orig(*a, **k)
+    eng._bn_train = boom
+    with pytest.raises(RuntimeError, match="injected"):
+        with torch.no_grad():
+            m(x)
+    eng._bn_train = orig
+    assert eng._zpool == {} and eng._nbt == []
+    # the failed forward updated the running stats of the first BNs: restore them from a fresh model
+    ref = DPTSegmentation(compute_dtype="bf16").cuda().train()
+    ref._rope_rescale = 1.1
+    m.load_state_dict(ref.state_dict())
+    with torch.no_grad():
+        a, b = m(x)["pred_masks"], ref(x)["pred_masks"]
+    # (equal up to the fp64 BN-sum atomics' summation order)
+    assert float((a - b).abs().max() / b.abs().max()) <= 1e-4
+    for (k, u), (_, v) in zip(m.named_buffers(), ref.named_buffers()):
+        assert torch.allclose(u.float(), v.float(), rtol=1e-5, atol=1e-6), k

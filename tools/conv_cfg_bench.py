@@ -53,11 +53,32 @@ def main():
     for kn in knobs:
         if kn is not None:
             os.environ["S3OD_CONV_PP"] = kn
+            os.environ["S3OD_WGRAD_PP"] = kn
         print(f"S3OD_CONV_PP={kn}", flush=True)
         run(B)
 
 
+def wgrad(tag, B, hh, Cin, Cout, relu=0):
+    g = torch.Generator(device="cuda").manual_seed(hh + Cin + 1)
+    dy = torch.randn(B, hh, hh, Cout, device="cuda", generator=g).bfloat16()
+    x = torch.randn(B, hh, hh, Cin, device="cuda", generator=g).bfloat16()
+    dw = torch.zeros(Cout, Cin, 3, 3, device="cuda")
+    ws = torch.zeros(Cout * 9 * Cin, device="cuda")
+    f = lambda: lib()("s3od_conv_wgrad", BF16, B, hh, hh, Cin, hh, hh, Cout, 3, 3, 1, 1, dy, x, relu, dw, ws, 0, stream())
+    t = timeit(f)
+    fl = 2.0 * B * hh * hh * Cin * Cout * 9
+    print(f"cfg={os.environ.get('S3OD_WGRAD_PP', 'def')} {tag:28s} {t * 1e6:8.1f} us {fl / t / 1e12:7.1f} TF/s", flush=True)
+
+
 def run(B):
+    if os.environ.get("WG"):
+        wgrad("wgrad rcu 256^2 relu", B, 256, 256, 256, relu=1)
+        wgrad("wgrad rcu 256^2", B, 256, 256, 256)
+        wgrad("wgrad rcu 128^2", B, 128, 256, 256)
+        wgrad("wgrad rn2 128^2 512", B, 128, 512, 256)
+        wgrad("wgrad rcu 64^2", B, 64, 256, 256)
+        wgrad("wgrad rn3 64^2 1024", B, 64, 1024, 256)
+        return
     conv("rcu 256^2 relu_in+stats", B, 256, 256, 256, relu_in=1, stats=True)
     conv("rcu 256^2 stats", B, 256, 256, 256, stats=True)
     conv("rcu/dgrad 256^2 plain", B, 256, 256, 256, bias=False)
