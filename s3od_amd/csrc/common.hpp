@@ -51,6 +51,10 @@ template <> DEV void load8<bf16>(const bf16* p, float* v) {
 #pragma unroll
   for (int i = 0; i < 8; i++) v[i] = (float)a[i];
 }
+template <typename T> DEV void store4(T* p, const float* v) {
+  if constexpr (sizeof(T) == 4) *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  else *(bf16x4*)p = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+}
 template <typename T> DEV void store8(T* p, const float* v);
 template <> DEV void store8<float>(float* p, const float* v) {
   *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);

@@ -104,29 +104,50 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const float* __restrict__ x
 
 // LayerNorm backward. dx = dres + rstd*(g - mean(g) - xhat*mean(g*xhat)), g = dy*w
 // dw += sum dy*xhat ; db += sum dy   (fp32 block partials -> replicated atomics [NREP][2D])
-template <typename T, int D>
+// LS: fused with the LayerScale backward of the layer below, which consumes this dx (ViT backward order:
+// norm2 -> layer_scale1 of the same layer, norm1 -> layer_scale2 of the next lower layer): du = dx * lam (T),
+// dlam += sum dx*u, dbias += sum du into a second replicated workspace ws2 -- saves that kernel's re-read of dx.
+template <typename T, int D, bool LS = false>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, const float* __restrict__ x,
                                                       const float* __restrict__ mean, const float* __restrict__ rstd,
                                                       const float* __restrict__ w, const float* __restrict__ dres,
                                                       float* __restrict__ dx, float* __restrict__ ws,
-                                                      int M, int rows_per_block) {
-  constexpr int NV = D / 256, NE = 4 * NV;
-  __shared__ float sdw[D], sdb[D];
-  for (int i = threadIdx.x; i < D; i += 256) { sdw[i] = 0.f; sdb[i] = 0.f; }
+                                                      int M, int rows_per_block, const T* __restrict__ u = nullptr,
+                                                      const float* __restrict__ lam = nullptr, T* __restrict__ du = nullptr,
+                                                      float* __restrict__ ws2 = nullptr) {
+  constexpr int NV = D / 256, NE = 4 * NV, NS = LS ? 4 : 2;
+  __shared__ float sred[NS][D];
+  float* sdw = sred[0];
+  float* sdb = sred[1];
+  for (int i = threadIdx.x; i < D; i += 256)
+#pragma unroll
+    for (int k = 0; k < NS; k++) sred[k][i] = 0.f;
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float pw[NE], pb[NE];
+  float pw[NE], pb[NE], pl[LS ? NE : 1], pd[LS ? NE : 1], lv[LS ? NE : 1];
 #pragma unroll
   for (int i = 0; i < NE; i++) { pw[i] = 0.f; pb[i] = 0.f; }
+  if constexpr (LS) {
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+      const float4 l4 = *(const float4*)(lam + 4 * (lane + 64 * i));
+      lv[4 * i] = l4.x; lv[4 * i + 1] = l4.y; lv[4 * i + 2] = l4.z; lv[4 * i + 3] = l4.w;
+    }
+#pragma unroll
+    for (int i = 0; i < NE; i++) { pl[i] = 0.f; pd[i] = 0.f; }
+  }
   int r0 = blockIdx.x * rows_per_block;
   for (int row = r0 + wave; row < min(M, r0 + rows_per_block); row += 4) {
     const float* xr = x + (long)row * D;
     float mu = mean[row], rs = rstd[row];
     float xh[NE], g[NE], dyv[NE];
     float4 rr4[NV];
+    bf16x4 uu4[LS ? NV : 1];
 #pragma unroll
-    for (int i = 0; i < NV; i++)   // issue the residual-gradient loads before the row reductions
+    for (int i = 0; i < NV; i++) {  // issue the residual-gradient (and LayerScale input) loads before the row reductions
       rr4[i] = dres ? *(const float4*)(dres + (long)row * D + 4 * (lane + 64 * i)) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (LS && sizeof(T) == 2) uu4[i] = *(const bf16x4*)(u + (long)row * D + 4 * (lane + 64 * i));
+    }
 #pragma unroll
     for (int i = 0; i < NV; i++) {
       int c = 4 * (lane + 64 * i);
@@ -157,6 +178,25 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
         pb[k] += dyv[k];
       }
       *(float4*)(dx + (long)row * D + c) = make_float4(o[0], o[1], o[2], o[3]);
+      if constexpr (LS) {
+        float uv[4];
+        if constexpr (sizeof(T) == 4) {
+          const float4 t = *(const float4*)(u + (long)row * D + c);
+          uv[0] = t.x; uv[1] = t.y; uv[2] = t.z; uv[3] = t.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; e++) uv[e] = (float)uu4[i][e];
+        }
+        float dd[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const int k = 4 * i + e;
+          dd[e] = o[e] * lv[k];
+          pl[k] += o[e] * uv[e];
+          pd[k] += dd[e];
+        }
+        store4<T>(du + (long)row * D + c, dd);
+      }
     }
   }
 #pragma unroll
@@ -167,9 +207,23 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
       atomicAdd(&sdw[c], pw[4 * i + e]);
       atomicAdd(&sdb[c], pb[4 * i + e]);
     }
+  if constexpr (LS) {
+#pragma unroll
+    for (int i = 0; i < NV; i++)
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        int c = 4 * (lane + 64 * i) + e;
+        atomicAdd(&sred[2][c], pl[4 * i + e]);
+        atomicAdd(&sred[3][c], pd[4 * i + e]);
+      }
+  }
   __syncthreads();
   float* rep = ws + (long)(blockIdx.x % S3OD_NREP) * 2 * D;   // replicated [dw | db] partials
   for (int i = threadIdx.x; i < D; i += 256) { atomicAdd(rep + i, sdw[i]); atomicAdd(rep + D + i, sdb[i]); }
+  if constexpr (LS) {
+    float* rep2 = ws2 + (long)(blockIdx.x % S3OD_NREP) * 2 * D;   // replicated [dlam | dbias] partials
+    for (int i = threadIdx.x; i < D; i += 256) { atomicAdd(rep2 + i, sred[2][i]); atomicAdd(rep2 + D + i, sred[3][i]); }
+  }
 }
 
 // a[i] += sum_r ws[r][i], b[i] += sum_r ws[r][D + i]   (fold of the replicated 2 x D partials; a/b may be null)
@@ -390,6 +444,26 @@ int s3od_layernorm_bwd(int dtype, const void* dy, const float* x, const float* m
   });
   hipLaunchKernelGGL(fold2_kernel, dim3(cdiv(2 * D_, 256)), dim3(256), 0, st, ws, dw, db, D_);
   return s3od_check_launch("layernorm_bwd");
+}
+
+// s3od_layernorm_bwd fused with the LayerScale backward (s3od_layerscale_bwd) of the layer that consumes its dx:
+// du = dx * lam, dlam += sum dx*u, dbias += sum du.  ws, ws2: S3OD_NREP * 2 * D floats each, all zero on entry and
+// left all zero.  Replaces the pair s3od_layernorm_bwd + s3od_layerscale_bwd (tf:modeling_dinov3_vit.py:419-445).
+int s3od_layernorm_ls_bwd(int dtype, const void* dy, const float* x, const float* mean, const float* rstd, const float* w,
+                          const float* dres, float* dx, float* dw, float* db, float* ws, const void* u, const float* lam,
+                          void* du, float* dlam, float* dbias, float* ws2, int M, int D_, void* stream) {
+  S3OD_REQUIRE(u && lam && du && ws2 && ws != ws2, "layernorm_ls_bwd: bad arguments");
+  static const int rpb = dev_knob("S3OD_LN_RPB", 32);
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_D(D_, {
+    DISPATCH_T(dtype, {
+      hipLaunchKernelGGL((ln_bwd_kernel<T, D, true>), dim3(cdiv(M, rpb)), dim3(256), 0, st, (const T*)dy, x, mean, rstd, w, dres,
+                         dx, ws, M, rpb, (const T*)u, lam, (T*)du, ws2);
+    });
+  });
+  hipLaunchKernelGGL(fold2_kernel, dim3(cdiv(2 * D_, 256)), dim3(256), 0, st, ws, dw, db, D_);
+  hipLaunchKernelGGL(fold2_kernel, dim3(cdiv(2 * D_, 256)), dim3(256), 0, st, ws2, dlam, dbias, D_);
+  return s3od_check_launch("layernorm_ls_bwd");
 }
 
 int s3od_cast_tap(int dtype, const float* x, void* y, int B, int Ntok, int P, int D, void* stream) {

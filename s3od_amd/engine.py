@@ -651,6 +651,8 @@ class DPTEngine:
         delta = _E(None, (B * H, Nt), torch.float32, dev)
         qv_ws = self.zero_ws("qv", 32 * 2 * D, torch.float32, dev)     # S3OD_NREP replicas of the q/v bias partials
         red_ws = self.zero_ws("red", 32 * 2 * D, torch.float32, dev)   # same, for LayerNorm / LayerScale parameter grads
+        red2_ws = self.zero_ws("red2", 32 * 2 * D, torch.float32, dev)  # the LayerScale half of the fused LN + LS backward
+        ls_done = False       # the layer's layer_scale2 backward already ran inside the layer above's norm1 backward
         for i in reversed(range(self.last)):
             if i + 1 in tap_of:
                 dp, c = dtaps[tap_of[i + 1]]
@@ -661,21 +663,22 @@ class DPTEngine:
             p = f"encoder.model.layer.{i}."
             s = ctx.t[f"L{i}"]
             # ---- MLP half
-            claim("du")
-            L("s3od_layerscale_bwd", dt, dx, s["u2"], P[p + "layer_scale2.lambda1"], du, G[p + "layer_scale2.lambda1"],
-              G[p + "mlp.down_proj.bias"], red_ws, M, D, st)
+            if not ls_done:
+                claim("du")
+                L("s3od_layerscale_bwd", dt, dx, s["u2"], P[p + "layer_scale2.lambda1"], du, G[p + "layer_scale2.lambda1"],
+                  G[p + "mlp.down_proj.bias"], red_ws, M, D, st)
             on_side(lambda: self._wgrad_lin(du, s["a"], D, MLP, M, G[p + "mlp.down_proj.weight"]), "du")
             claim("dhp")
             self._dgrad_lin(du, W8[f"down{i}"], M, MLP, D, dhp, act=ACT_MUL if dt == BF16 else ACT_GELU_BWD, aux=s["hpre"],
                             colsum=G[p + "mlp.up_proj.bias"])
             on_side(lambda: self._wgrad_lin(dhp, s["h2"], MLP, D, M, G[p + "mlp.up_proj.weight"]), "dhp")
             self._dgrad_lin(dhp, W8[f"up{i}"], M, D, MLP, dh)
-            L("s3od_layernorm_bwd", dt, dh, s["xm"], s["mean2"], s["rstd2"], P[p + "norm2.weight"], dx, dxm,
-              G[p + "norm2.weight"], G[p + "norm2.bias"], red_ws, M, D, st)
-            # ---- attention half
+            # norm2 backward fused with the attention half's layer_scale1 backward (which reads its dxm)
             claim("du2")
-            L("s3od_layerscale_bwd", dt, dxm, s["u1"], P[p + "layer_scale1.lambda1"], du2, G[p + "layer_scale1.lambda1"],
-              G[p + "attention.o_proj.bias"], red_ws, M, D, st)
+            L("s3od_layernorm_ls_bwd", dt, dh, s["xm"], s["mean2"], s["rstd2"], P[p + "norm2.weight"], dx, dxm,
+              G[p + "norm2.weight"], G[p + "norm2.bias"], red_ws, s["u1"], P[p + "layer_scale1.lambda1"], du2,
+              G[p + "layer_scale1.lambda1"], G[p + "attention.o_proj.bias"], red2_ws, M, D, st)
+            # ---- attention half
             on_side(lambda: self._wgrad_lin(du2, s["o"], D, D, M, G[p + "attention.o_proj.weight"]), "du2")
             do = dh
             self._dgrad_lin(du2, W8[f"o{i}"], M, D, D, do)
@@ -686,8 +689,17 @@ class DPTEngine:
             on_side(lambda: self._wgrad_lin(dqkv, s["h1"], 3 * D, D, M, G[f"qkv_w{i}"]), "dqkv")
             dh1 = dh
             self._dgrad_lin(dqkv, W8[f"qkv{i}"], M, D, 3 * D, dh1)
-            L("s3od_layernorm_bwd", dt, dh1, s["x"], s["mean1"], s["rstd1"], P[p + "norm1.weight"], dxm, dxi,
-              G[p + "norm1.weight"], G[p + "norm1.bias"], red_ws, M, D, st)
+            # norm1 backward, fused with layer i-1's layer_scale2 backward unless a tap gradient joins dx in between
+            ls_done = i >= 1 and i not in tap_of
+            if ls_done:
+                q = f"encoder.model.layer.{i - 1}."
+                claim("du")
+                L("s3od_layernorm_ls_bwd", dt, dh1, s["x"], s["mean1"], s["rstd1"], P[p + "norm1.weight"], dxm, dxi,
+                  G[p + "norm1.weight"], G[p + "norm1.bias"], red_ws, ctx.t[f"L{i - 1}"]["u2"], P[q + "layer_scale2.lambda1"],
+                  du, G[q + "layer_scale2.lambda1"], G[q + "mlp.down_proj.bias"], red2_ws, M, D, st)
+            else:
+                L("s3od_layernorm_bwd", dt, dh1, s["x"], s["mean1"], s["rstd1"], P[p + "norm1.weight"], dxm, dxi,
+                  G[p + "norm1.weight"], G[p + "norm1.bias"], red_ws, M, D, st)
             dx, dxi = dxi, dx
             if self.grad_hook is not None:
                 # the layer's gradients are final once both streams are past it: the hook (the DDP bucket all-reduce)

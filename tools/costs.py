@@ -57,6 +57,9 @@ def cost(name, a):
     if n == "layernorm_bwd":
         dt, dres, M = a[0], a[6], a[11]
         return "hbm", M * D * (_t(dt) + 4 + 4 + (4 if dres is not None else 0)) + 8.0 * M
+    if n == "layernorm_ls_bwd":       # the LayerNorm backward + the LayerScale backward's u read and du write
+        dt, dres, M = a[0], a[6], a[17]
+        return "hbm", M * D * (_t(dt) + 4 + 4 + (4 if dres is not None else 0) + 2 * _t(dt)) + 8.0 * M
     if n == "layerscale_bwd":
         dt, M = a[0], a[8]
         return "hbm", M * D * (4 + 2 * _t(dt))
