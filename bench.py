@@ -423,7 +423,15 @@ def main():
     bd = None
     dom = "s3od_attn_bwd_qkv" if args.mode == "train" else "s3od_attn_fwd"
     if not args.no_breakdown:
-        dom, bd = breakdown(step, 2, peak)
+        # per-entry times are measured with the backward on ONE stream: beside the side-stream weight gradients every
+        # kernel shares the CUs and its own duration stretches (the timed region below keeps the two streams)
+        os.environ["S3OD_BWD_SIDE"] = "0"
+        try:
+            dom, bd = breakdown(step, 2, peak)
+        finally:
+            os.environ.pop("S3OD_BWD_SIDE", None)
+        bd["note"] = ("per-entry GPU times from a separate 2-step pass with the encoder backward on one stream (the timed "
+                      "region runs the weight gradients on a side stream beside the data-gradient chain)")
     torch.cuda.synchronize()
     log(f"timed region: {args.steps} steps, roofline entry {dom}")
     from tools.costs import cost

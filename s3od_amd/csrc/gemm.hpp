@@ -1125,16 +1125,6 @@ __global__ void __launch_bounds__(GEMM_THREADS, 1) igemm_pp_kernel(LA la0, LB lb
   lb0.setup(n0, tid); lb1.setup(n0 + 128, tid);
   constexpr int NA = LA::NIW * 2;              // DMA instructions per wave for the two A halves
   const bool stag = !(flags & 1);              // dev knob S3OD_PP_FLAGS bit 0: no stagger
-  // CU desynchronisation (flags >> 8 = delay in units of 1024 cycles): every tile of a launch takes the same time, so
-  // the first round's workgroups reach their store-heavy epilogues together and every later round inherits that
-  // lock-step.  Delaying half of the first round (every other workgroup of each XCD) offsets the CUs' tile rounds so
-  // one half's epilogue stores run under the other half's main loop.
-  if (const int dl = flags >> 8) {
-    const int L = blockIdx.y * gridDim.x + blockIdx.x;
-    if (L < 256 && ((L >> 3) & 1))
-      for (int c = 0; c < dl; c++) __builtin_amdgcn_s_sleep(16);
-  }
-
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; i++)
@@ -1236,9 +1226,7 @@ static int launch_igemm(LA la, LB lb, EPI epi, int M, int N, int KTILES, int spl
     auto kfn = igemm_pp_kernel<LA, LB, EPI>;
     static bool attr = false;
     if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS); attr = true; }
-    static const int flags0 = dev_knob("S3OD_PP_FLAGS", 0);
-    const char* sd = getenv("S3OD_PP_STAGGER");      // per call: first-round delay (x 1024 cycles) for A/B runs
-    const int flags = flags0 | ((sd ? atoi(sd) : 0) << 8);
+    static const int flags = dev_knob("S3OD_PP_FLAGS", 0);
     dim3 grid(cdiv(N, BN), cdiv(M, BM), split * zdim_extra);
     hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), PP_LDS, st, la, lb, epi, KTILES, split, flags);
     return s3od_check_launch("igemm_pp");

@@ -1522,10 +1522,13 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
     return s3od_check_launch("conv_wgrad permute");
   }
   if (dtype == S3OD_BF16 && ws && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && W % 64 == 0 &&
-      Cin % 256 == 0 && Cout % 256 == 0 && tl_cfg < 0 && gemm_cfg() < 0 && !getenv_zero("S3OD_WGRAD_PP")) {
+      Cin % 256 == 0 && Cout % 256 == 0 && ((long)H * W >= 128L * 128 || Cin >= 512) && tl_cfg < 0 && gemm_cfg() < 0 &&
+      !getenv_zero("S3OD_WGRAD_PP")) {
     // the 256-channel RCU / layerK_rn weight gradients on the ping-pong kernel: one 256 x 256 tile = 256 output
     // channels x one tap's 256 input channels, K = pixels split over ~one round of workgroups (fp32 atomics into the
-    // GEMM-layout workspace, then the permute into dW)
+    // GEMM-layout workspace, then the permute into dW).  Measured vs the 128x128 implicit GEMM (tools/conv_cfg_bench.py
+    // WG=1, bs 16): 256^2 1.47 vs 1.63-1.66 ms (ReLU'd input 1.52 vs 1.77-1.97), 128^2 0.39 vs 0.42, 128^2 512 -> 256
+    // 0.76 vs 0.85, 64^2 1024 -> 256 0.38 vs 0.44; the 64^2 256 -> 256 one (0.14 vs 0.13 ms) stays on 128x128
     const int KTILES = NPIX / 64, tiles = (Cout / 256) * (N / 256);
     int sp = split > 0 ? split : std::max(1, std::min(256 / tiles, KTILES / 8));
     DenseMC<bf16, 128> la{(const bf16*)dy, (long)Cout, NPIX, Cout};

@@ -102,24 +102,11 @@ def heads(name, B, H):
 
 
 def report(name, fl, t):
-    tag = os.environ.get('S3OD_GEMM_CFG', 'def') + "/st" + os.environ.get("S3OD_PP_STAGGER", "0")
-    print(f"cfg {tag:>7} {name:40s} {t * 1e6:8.1f} us {fl / t / 1e12:7.1f} TF/s", flush=True)
+    tag = os.environ.get('S3OD_GEMM_CFG', 'def')
+    print(f"cfg {tag:>3} {name:40s} {t * 1e6:8.1f} us {fl / t / 1e12:7.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
-    if os.environ.get("SWEEP") == "stagger":
-        # the ping-pong kernel's first-round CU offset (S3OD_PP_STAGGER, x 1024 cycles, read per call)
-        for rnd in range(2):
-            for st in (sys.argv[1:] or ["0", "6", "12"]):
-                os.environ["S3OD_PP_STAGGER"] = st
-                qkv()
-                fwd("o_proj fwd N768 K768 (res f32, out f32, pre)", D, D, res_f32=True, out_f32=True, pre=True, scale=True)
-                fwd("up fwd N3072 K768 (GELU, gelu' saved)", F, D, act=5, pre=True)
-                fwd("down fwd N768 K3072 (res f32, out f32, pre)", D, F, res_f32=True, out_f32=True, pre=True, scale=True)
-                dgrad("up dgrad N768 K3072", D, F)
-                wgrad("wgrad 3072x768", F, D)
-                conv("conv fwd 256->256 3x3 @256^2 bs16", 16, 256, 256, 256)
-        sys.exit(0)
     if os.environ.get("SWEEP") == "conv256":
         for hh in (256, 128, 64):
             conv(f"conv fwd 256->256 3x3 @{hh}^2 bs16", 16, hh, 256, 256)
