@@ -1043,6 +1043,24 @@ struct EpiWgrad {
   }
 };
 
+// split-K wgrad epilogue without atomics: split z writes its whole fp32 tile to its own slab ws[z][M][N] with 16-B
+// stores (every workgroup writes its tile, an empty K range writes zeros), and wgrad_reduce_kernel sums the slabs into
+// dW.  The fp32 atomics of EpiWgrad run at the chip's ~1.3 TB/s atomic rate and all land at the end of every workgroup
+// (one round); plain stores move the same bytes at the store rate.
+struct EpiWgradPart {
+  float* ws; int M, N;
+  int z = 0;
+  DEV void prepare(int zz) { z = zz; }
+  DEV void operator()(const float* ct, int LDT, int m0, int n0, int tid, int BM, int BN, int NT) const {
+    float* slab = ws + (long)z * M * N;
+    for_segments(ct, LDT, BM, BN, m0, n0, M, N, tid, NT, [&](int m, int n, const float* a, int, int) {
+      float4* d = (float4*)(slab + (long)m * N + n);
+      d[0] = make_float4(a[0], a[1], a[2], a[3]);
+      d[1] = make_float4(a[4], a[5], a[6], a[7]);
+    });
+  }
+};
+
 // ------------------------------------------------------------------ 256x256 ping-pong kernel (bf16)
 // 8 waves = 2 (M) x 4 (N), each owning a 128x64 sub-tile (acc[8][4], 128 VGPRs); waves w and w+4
 // share a SIMD (cyclic wave->SIMD placement), so the two M halves are SIMD partners.  The M half

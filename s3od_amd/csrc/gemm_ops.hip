@@ -1181,6 +1181,59 @@ template <typename T, int BM, int BN, int NST> static int wgrad_split(int tiles,
   return best;
 }
 
+// dW (+)= the sum of the split-K slabs ws[sp][M][N] (EpiWgradPart), scattered to the PyTorch layout
+// dW[(m*Cx + cin)*taps + tap] for n = tap*Cx + cin (Linear: taps = 1, Cx = N).  One thread per 4 consecutive n.
+__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int sp, int M, int N, float* __restrict__ dw, int Cx, int taps) {
+  const long i4 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const long MN = (long)M * N;
+  if (i4 >= MN) return;
+  float4 s = *(const float4*)(ws + i4);
+  for (int z = 1; z < sp; z++) {
+    const float4 v = *(const float4*)(ws + (long)z * MN + i4);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  const int m = (int)(i4 / N), n = (int)(i4 - (long)m * N);
+  if (taps == 1) {
+    float4* d = (float4*)(dw + i4);
+    const float4 o = *d;
+    *d = make_float4(o.x + s.x, o.y + s.y, o.z + s.z, o.w + s.w);
+    return;
+  }
+  const float sv[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const int tap = (n + e) / Cx, cin = (n + e) - tap * Cx;
+    dw[((long)m * Cx + cin) * taps + tap] += sv[e];
+  }
+}
+
+// per-stream scratch for the split-K slabs (grown on demand, kept for the process; calls on one stream run in order,
+// so a stream's slab is free again once its reduce kernel has run)
+static float* slab_scratch(hipStream_t st, size_t bytes) {
+  struct Ent { hipStream_t st; float* p; size_t n; };
+  static Ent tab[8] = {};
+  for (auto& e : tab) {
+    if (e.p && e.st == st) {
+      if (e.n >= bytes) return e.p;
+      (void)hipStreamSynchronize(st);
+      (void)hipFree(e.p);
+      e.p = nullptr;
+      if (hipMalloc((void**)&e.p, bytes) != hipSuccess) { e.p = nullptr; return nullptr; }
+      e.n = bytes;
+      return e.p;
+    }
+  }
+  for (auto& e : tab)
+    if (!e.p) {
+      if (hipMalloc((void**)&e.p, bytes) != hipSuccess) return nullptr;
+      e.st = st; e.n = bytes;
+      return e.p;
+    }
+  return nullptr;
+}
+// S3OD_WGRAD_SLAB=0 (read per call): the fp32-atomic split-K epilogue instead of the slabs (A/B)
+static bool slab_ok() { return !getenv_zero("S3OD_WGRAD_SLAB"); }
+
 // dw[(co*Cin + ci)*taps + tap] += ws[(co*taps + tap)*Cin + ci]   (one thread per dw element)
 // ws enters all zero (split-K atomics land in it) and leaves all zero: each element is cleared as it is read,
 // so a persistent workspace needs no memset per call
@@ -1304,7 +1357,19 @@ int s3od_linear_wgrad(int dtype, int Nout, int Kin, int rows, const void* dy, lo
       int sp = split > 0 ? split : wgrad_split<T, BM, BN, NST>(cdiv(Nout, BM) * cdiv(Kin, BN), KTILES);
       DenseMC<T, decltype(C)::LM, decltype(C)::W> la{(const T*)dy, lddy, rows, Nout};
       DenseMC<T, decltype(C)::LN, decltype(C)::W> lb{(const T*)x, ldx, rows, Kin};
+      if constexpr (decltype(C)::PP) {
+        float* slab = (slab_ok() && sp > 1 && Kin % 4 == 0) ? slab_scratch(st, (size_t)sp * Nout * Kin * 4) : nullptr;
+        if (slab) {
+          EpiWgradPart e{slab, Nout, Kin};
+          int rc = launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, Nout, Kin, KTILES, sp, 1, st);
+          if (rc) return rc;
+          hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv((long)Nout * Kin / 4, 256)), dim3(256), 0, st, slab, sp, Nout, Kin, dw, Kin, 1);
+          return s3od_check_launch("linear_wgrad reduce");
+        }
+      }
       EpiWgrad e{dw, Nout, Kin, Kin, 1};
+      static const int epi_probe = dev_knob("S3OD_EPI_PROBE", 0);   // dev: 1 = skip the split-K atomics (timing only)
+      if (epi_probe == 1) e.M = 0;
       return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, Nout, Kin, KTILES, sp, 1, st);
     });
   });
@@ -1532,12 +1597,20 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
     const int KTILES = NPIX / 64, tiles = (Cout / 256) * (N / 256);
     int sp = split > 0 ? split : std::max(1, std::min(256 / tiles, KTILES / 8));
     DenseMC<bf16, 128> la{(const bf16*)dy, (long)Cout, NPIX, Cout};
-    EpiWgrad e{ws, M, N, N, 1};
-    auto pp = [&](auto rl) -> int {
+    float* slab = (slab_ok() && sp > 1) ? slab_scratch(st, (size_t)sp * M * N * 4) : nullptr;
+    auto pp = [&](auto rl, auto e) -> int {
       Wgrad3B<128, decltype(rl)::value> lb{}; lb.x = (const bf16*)x; lb.B = B; lb.H = H; lb.W = W; lb.Cin = Cin;
       return launch_igemm<bf16, 256, 256, decltype(la), decltype(lb), decltype(e)>(la, lb, e, M, N, KTILES, sp, 1, st);
     };
-    int rc = relu_x ? pp(std::true_type{}) : pp(std::false_type{});
+    if (slab) {       // split-K slabs, summed straight into dW's PyTorch layout (the atomic workspace stays untouched)
+      EpiWgradPart e{slab, M, N};
+      int rc = relu_x ? pp(std::true_type{}, e) : pp(std::false_type{}, e);
+      if (rc) return rc;
+      hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv((long)M * N / 4, 256)), dim3(256), 0, st, slab, sp, M, N, dw, Cin, KH * KW);
+      return s3od_check_launch("conv_wgrad reduce");
+    }
+    EpiWgrad e{ws, M, N, N, 1};
+    int rc = relu_x ? pp(std::true_type{}, e) : pp(std::false_type{}, e);
     if (rc) return rc;
     hipLaunchKernelGGL(wgrad_permute_add_kernel, dim3(cdiv((long)M * N, 256)), dim3(256), 0, st, ws, dw, M, Cin, KH * KW);
     return s3od_check_launch("conv_wgrad permute");

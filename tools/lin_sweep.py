@@ -107,6 +107,25 @@ def report(name, fl, t):
 
 
 if __name__ == "__main__":
+    if os.environ.get("SWEEP") == "ab":
+        # same-process A/B of a per-call knob: KNOB=<env name>, positional values (e.g. S3OD_PP_DMA 0 1)
+        knob = os.environ["KNOB"]
+        for rnd in range(2):
+            for val in sys.argv[1:]:
+                os.environ[knob] = val
+                print(f"--- {knob}={val} round {rnd}", flush=True)
+                qkv()
+                fwd("o_proj fwd N768 K768 (res f32, out f32, pre)", D, D, res_f32=True, out_f32=True, pre=True, scale=True)
+                fwd("up fwd N3072 K768 (GELU, gelu' saved)", F, D, act=5, pre=True)
+                fwd("down fwd N768 K3072 (res f32, out f32, pre)", D, F, res_f32=True, out_f32=True, pre=True, scale=True)
+                dgrad("up dgrad N768 K3072", D, F)
+                dgrad("qkv dgrad N768 K2304", D, 3 * D)
+                wgrad("wgrad 3072x768", F, D)
+                wgrad("wgrad 768x3072", D, F)
+                wgrad("wgrad 2304x768", 3 * D, D)
+                conv("conv fwd 256->256 3x3 @256^2 bs16", 16, 256, 256, 256)
+                wgrad_conv("conv wgrad 256x(3x3x256) @256^2 bs16", 16, 256, 256, 256)
+        sys.exit(0)
     if os.environ.get("SWEEP") == "conv256":
         for hh in (256, 128, 64):
             conv(f"conv fwd 256->256 3x3 @{hh}^2 bs16", 16, hh, 256, 256)
