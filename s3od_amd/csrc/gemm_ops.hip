@@ -1234,6 +1234,51 @@ static float* slab_scratch(hipStream_t st, size_t bytes) {
 // S3OD_WGRAD_SLAB=0 (read per call): the fp32-atomic split-K epilogue instead of the slabs (A/B)
 static bool slab_ok() { return !getenv_zero("S3OD_WGRAD_SLAB"); }
 
+// M-tail launches (split_tail: the <= 255 rows past the last full 256-row panel, on 128x128 tiles): a tail has only
+// N/128 tiles (6 for N 768), each a full-K main loop on an otherwise idle chip (35-45 us at K 3072).  Split-K instead:
+// sp K ranges write fp32 slabs [sp][M][N] (EpiWgradPart), then tail_epi_kernel sums them per 16 x 128 tile in LDS and
+// runs the op's own epilogue functor on the sum (bias / scale / act / residuals / pre / column sums, unchanged).
+// S3OD_TAIL_SK=0 (read per call): the single full-K tail launch.
+template <class EPI>
+__global__ void __launch_bounds__(256) tail_epi_kernel(const float* __restrict__ ws, int sp, int M, int N, EPI epi) {
+  constexpr int TM = 16, TN = 128, LDT = TN + 4;
+  __shared__ __attribute__((aligned(16))) float ct[TM * LDT];     // also the column-sum reduction's 256 x 8 floats
+  const int tid = threadIdx.x, m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
+  const int r = tid >> 4, c = (tid & 15) * 8;
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (m0 + r < M && n0 + c < N) {
+    const float* p = ws + (long)(m0 + r) * N + n0 + c;
+    for (int z = 0; z < sp; z++, p += (long)M * N) {
+      const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+  }
+  *(float4*)(ct + r * LDT + c) = make_float4(v[0], v[1], v[2], v[3]);
+  *(float4*)(ct + r * LDT + c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  __syncthreads();
+  epi.prepare(0);
+  epi(ct, LDT, m0, n0, tid, TM, TN, 256);
+}
+template <typename T, int BM, int BN, int NST, int WM, class LA, class LB, class EPI>
+static int launch_tail(LA la, LB lb, EPI e, int M, int N, int KTILES, hipStream_t st) {
+  const int tiles = cdiv(M, BM) * cdiv(N, BN), sp = std::min(256 / tiles, KTILES / 4);
+  float* ws = (sp >= 2 && M < 256 && N % 8 == 0 && !getenv_zero("S3OD_TAIL_SK")) ? slab_scratch(st, (size_t)sp * M * N * 4)
+                                                                               : nullptr;
+  if (!ws) return launch_igemm<T, BM, BN, LA, LB, EPI, NST, WM>(la, lb, e, M, N, KTILES, 1, 1, st);
+  EpiWgradPart part{ws, M, N};
+  int rc = launch_igemm<T, BM, BN, LA, LB, EpiWgradPart, NST, WM>(la, lb, part, M, N, KTILES, sp, 1, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(tail_epi_kernel<EPI>, dim3(cdiv(N, 128), cdiv(M, 16)), dim3(256), 0, st, ws, sp, M, N, e);
+  return s3od_check_launch("igemm tail epilogue");
+}
+// the launch of one with_cfg config: the M-tail form (split-K) when this is a tail launch on 128x128 tiles
+template <typename T, class C, class LA, class LB, class EPI>
+static int launch_op(LA la, LB lb, EPI e, int M, int N, int KTILES, hipStream_t st) {
+  if constexpr (!C::PP)
+    if (tl_cfg == 1) return launch_tail<T, C::BM, C::BN, C::NST, C::WM>(la, lb, e, M, N, KTILES, st);
+  return launch_igemm<T, C::BM, C::BN, LA, LB, EPI, C::NST, C::WM>(la, lb, e, M, N, KTILES, 1, 1, st);
+}
+
 // dw[(co*Cin + ci)*taps + tap] += ws[(co*taps + tap)*Cin + ci]   (one thread per dw element)
 // ws enters all zero (split-K atomics land in it) and leaves all zero: each element is cleared as it is read,
 // so a persistent workspace needs no memset per call
@@ -1292,7 +1337,7 @@ int s3od_linear_fwd(int dtype, int M, int N, int K, const void* x, long ldx, con
                             (T*)pre, ldp, nullptr, act, M, N, rm};
         static const int epi_probe = dev_knob("S3OD_EPI_PROBE", 0);   // dev: 1 = skip the epilogue's stores
         if (epi_probe == 1) e.M = 0;
-        return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, M, N, KTILES, 1, 1, st);
+        return launch_op<T, decltype(C)>(la, lb, e, M, N, KTILES, st);
       });
     };
     if (out_f32 && res_f32) return go(0, float{}, float{});
@@ -1333,10 +1378,10 @@ int s3od_linear_dgrad(int dtype, int M, int N, int K, const void* dy, long lddy,
       if (out_f32) {
         // f32 output: aux is an f32 tensor to add (e.g. the residual-stream gradient, in place)
         EpiStd<float, float> e{(float*)dx, lddx, 0, nullptr, nullptr, nullptr, (const float*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, rm, colsum};
-        return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, M, N, KTILES, 1, 1, st);
+        return launch_op<T, decltype(C)>(la, lb, e, M, N, KTILES, st);
       }
       EpiStd<T, T> e{(T*)dx, lddx, 0, nullptr, nullptr, nullptr, (const T*)aux, ldaux, nullptr, 0, nullptr, 0, nullptr, act, M, N, rm, colsum};
-      return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, M, N, KTILES, 1, 1, st);
+      return launch_op<T, decltype(C)>(la, lb, e, M, N, KTILES, st);
     });
   });
   return 0;
@@ -1389,7 +1434,7 @@ int s3od_qkv_rope_fwd(int dtype, int B, int Ntok, int P, int H, const void* x, c
         DenseKC<T, decltype(C)::LN, decltype(C)::W> lb{(const T*)w, (long)D, N, D, 0};
         EpiQKV<T> e{(T*)q, (T*)k, (T*)v, bias, cos_t, sin_t, M, Ntok, P, H};
         e.moff = m_first;
-        return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, M, N, cdiv(D, KT<T>::BK), 1, 1, st);
+        return launch_op<T, decltype(C)>(la, lb, e, M, N, cdiv(D, KT<T>::BK), st);
       });
     };
     if (!split_tail(Mall)) return part(0, Mall);

@@ -223,3 +223,35 @@ def test_pp_production_rows_65616():
     L("s3od_linear_wgrad", BF16, F, D, M, dh, F, x, D, dw, 0, s)
     torch.cuda.synchronize()
     assert rel_l2(dw, dw0 + dh.float().t() @ x.float()) < 1e-5
+
+
+@pytest.mark.parametrize("tail_sk", ["1", "0"])
+def test_pp_tail_split_k_epilogues(tail_sk, monkeypatch):
+    """The M-tail launch as split-K (fp32 slabs summed by tail_epi_kernel, which then runs the op's own epilogue) and
+    as the single full-K launch (S3OD_TAIL_SK=0): GELU'-multiplied dgrad with the column sums the engine uses for bias
+    gradients (fp32 atomics), the o_proj form (bias, LayerScale, fp32 residual, pre) and QKV + RoPE, each over
+    65536 + 80 rows (K 3072 / 768), checked on the tail rows and the column sums against fp32 torch."""
+    monkeypatch.setenv("S3OD_TAIL_SK", tail_sk)
+    torch.manual_seed(80)
+    L, s = _lib()
+    M, D, F = 65536 + 80, 768, 3072
+    # down-projection dgrad: dx = (dy w) * g (ACT_MUL, g = saved gelu'), colsum += sum_m dx
+    dy, w, g = r(M, D), r(D, F, scale=D ** -0.5), r(M, F)
+    dx = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
+    cs = torch.zeros(F, device="cuda")
+    L("s3od_linear_dgrad", BF16, M, F, D, dy, D, w, 6, g, F, dx, F, 0, 0, 0, 0, cs, s)
+    ref = (dy.float() @ w.float()) * g.float()
+    torch.cuda.synchronize()
+    assert rel_l2(dx[-80:].float(), ref[-80:]) < 4e-3 and rel_l2(dx.float(), ref) < 4e-3
+    assert rel_l2(cs, ref.sum(0)) < 1e-4          # the column sums are of the fp32 values, before the bf16 store
+    del dy, w, g, dx, ref
+    # o_proj forward: out_f32 = (x w^T + b) * ls + res, pre stored; K 3072 (down-projection shape)
+    x, w, b, ls = r(M, F), r(D, F, scale=F ** -0.5), r(D, dt=torch.float32), r(D, dt=torch.float32)
+    res = r(M, D, dt=torch.float32)
+    out = torch.empty(M, D, device="cuda")
+    pre = torch.empty(M, D, device="cuda", dtype=torch.bfloat16)
+    L("s3od_linear_fwd", BF16, M, D, F, x, F, w, b, ls, None, 0, res, D, None, 0, 1, out, D, 1, pre, D, 0, 0, 0, s)
+    p = x.float() @ w.float().t() + b
+    torch.cuda.synchronize()
+    assert rel_l2(out[-80:], p[-80:] * ls + res[-80:]) < 1e-5
+    assert rel_l2(pre[-80:].float(), p[-80:]) < 4e-3

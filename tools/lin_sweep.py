@@ -12,7 +12,7 @@ import torch
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 from s3od_amd._lib import lib, stream, BF16  # noqa: E402
 
-M, D, F = 65616, 768, 3072
+M, D, F = int(os.environ.get("LIN_M", 65616)), 768, 3072   # LIN_M: row count (tail studies)
 ACT_GELU, ACT_GELU_BWD = 2, 3
 
 
@@ -125,6 +125,20 @@ if __name__ == "__main__":
                 wgrad("wgrad 2304x768", 3 * D, D)
                 conv("conv fwd 256->256 3x3 @256^2 bs16", 16, 256, 256, 256)
                 wgrad_conv("conv wgrad 256x(3x3x256) @256^2 bs16", 16, 256, 256, 256)
+        sys.exit(0)
+    if os.environ.get("SWEEP") == "tail":
+        # cost of the 80-row M tail: the fwd / dgrad shapes at 65536 rows (whole panels), 65616 (+ tail launch) and
+        # the tail alone (80 rows; S3OD_GEMM_CFG selects its config)
+        for m in (65536, 65616, 80, 65536, 65616, 80):
+            M = m
+            print(f"--- M={m}", flush=True)
+            fwd("o_proj fwd N768 K768 (res f32, out f32, pre)", D, D, res_f32=True, out_f32=True, pre=True, scale=True)
+            fwd("up fwd N3072 K768 (GELU, gelu' saved)", F, D, act=5, pre=True)
+            fwd("down fwd N768 K3072 (res f32, out f32, pre)", D, F, res_f32=True, out_f32=True, pre=True, scale=True)
+            dgrad("up dgrad N768 K3072", D, F)
+            dgrad("down dgrad N3072 K768 (gelu')", F, D, act=6, aux=True)
+            dgrad("qkv dgrad N768 K2304", D, 3 * D)
+            dgrad("o_proj dgrad N768 K768", D, D)
         sys.exit(0)
     if os.environ.get("SWEEP") == "conv256":
         for hh in (256, 128, 64):
