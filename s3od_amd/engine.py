@@ -349,9 +349,10 @@ class DPTEngine:
               self.buf[name + ".running_var"], 1e-5, s, t, 256, st)
         return s, t
 
-    def _fusion(self, r, x0, x1, B, h, w, oh, ow, train, ctx):
+    def _fusion(self, r, x0, x1, B, h, w, oh, ow, train, ctx, pre_resize=None):
         """FeatureFusionBlock (src/s3od/model.py:383-405). out_conv (1x1, bias) runs before the
-        bilinear resize: both are linear and bilinear weights sum to one, so the order commutes."""
+        bilinear resize: both are linear and bilinear weights sum to one, so the order commutes.
+        pre_resize: a list that receives the tensor before the resize (the classifier's pooled input)."""
         P, W8 = self.p, self.w
         s = x0 if x1 is None else self._rcu(x1, r, 1, B, h, w, train, ctx, x0=x0)
         s = self._rcu(s, r, 2, B, h, w, train, ctx)
@@ -360,6 +361,8 @@ class DPTEngine:
         self._lin(s, W8[f"ref{r}.out"], B * h * w, 256, 256, c, bias=P[q + "out_conv.bias"])
         if ctx is not None:
             ctx.t[f"ref{r}"] = dict(s=s, h=h, w=w, oh=oh, ow=ow)
+        if pre_resize is not None:
+            pre_resize.append(c)
         return self._bilinear(c, B, h, w, oh, ow, 256)
 
     def decoder_forward(self, taps, B, ph, pw, train=False, ctx=None):
@@ -386,11 +389,18 @@ class DPTEngine:
         p4 = self._fusion(4, rn[3], None, B, *dims[3], *dims[2], train, ctx)
         p3 = self._fusion(3, p4, rn[2], B, *dims[2], *dims[1], train, ctx)
         p2 = self._fusion(2, p3, rn[1], B, *dims[1], *dims[0], train, ctx)
-        p1 = self._fusion(1, p2, rn[0], B, *dims[0], 2 * dims[0][0], 2 * dims[0][1], train, ctx)
+        c1 = []
+        p1 = self._fusion(1, p2, rn[0], B, *dims[0], 2 * dims[0][0], 2 * dims[0][1], train, ctx, pre_resize=c1)
         H1, W1 = p1.shape[1], p1.shape[2]
-        # classifier head: AdaptiveAvgPool2d(1) -> Linear -> ReLU -> Linear
+        # classifier head: AdaptiveAvgPool2d(1) -> Linear -> ReLU -> Linear.  The mean of p1 is taken over the
+        # tensor BEFORE refinenet1's 2x bilinear resize (align_corners=False): every source pixel's weights over
+        # the 4x outputs sum to 4 (edge rows / columns included: clamped taps add up to the same 2 per axis), so
+        # mean(up2(c)) = mean(c) exactly in real arithmetic, read from a 4x smaller tensor (C5: 2.2 -> 0.55 GB)
         pooled = torch.empty((B, 256), dtype=torch.float32, device=dev)
-        L("s3od_avgpool", dt, p1, pooled, B, H1 * W1, 256, st)
+        if os.environ.get("S3OD_POOL_PRE", "1") != "0":     # (A/B: 0 = pool p1 itself)
+            L("s3od_avgpool", dt, c1[0], pooled, B, dims[0][0] * dims[0][1], 256, st)
+        else:
+            L("s3od_avgpool", dt, p1, pooled, B, H1 * W1, 256, st)
         hid = torch.empty((B, 64), dtype=torch.float32, device=dev)
         nm = self.nm
         iou = torch.empty((B, nm), dtype=torch.float32, device=dev)

@@ -2,6 +2,7 @@
 settings of one per-call environment knob, alternating rounds (dev tool).
 
     python tools/ab_step.py S3OD_BWD_SIDE 0 1 [rounds] [steps]
+    AB_MODE=infer AB_BATCH=8 AB_SIZE=1024 python tools/ab_step.py S3OD_POOL_PRE 0 1   # eval forward (C2 / C5)
 """
 import os
 import sys
@@ -22,12 +23,18 @@ def main():
     from s3od_amd.loss import LossModule, FOCAL_IOU
     from s3od_amd.optim import FusedAdamW, reference_param_groups
     dev = torch.device("cuda", 0)
-    m = DPTSegmentation(compute_dtype="bf16").to(dev).train()
+    infer = os.environ.get("AB_MODE") == "infer"
+    m = DPTSegmentation(compute_dtype="bf16").to(dev)
+    m.eval() if infer else m.train()
     crit = LossModule(FOCAL_IOU, full_mask_lambda=0.1, decay_rate=0.2)
     opt = FusedAdamW(reference_param_groups(m, 1e-5), weight_decay=0.05)
-    x, masks = synthetic_batch(16, 1024, 1000, dev)
+    x, masks = synthetic_batch(int(os.environ.get("AB_BATCH", 8 if infer else 16)), int(os.environ.get("AB_SIZE", 1024)),
+                               1000, dev)
 
     def step():
+        if infer:
+            with torch.no_grad():
+                return m(x)["pred_iou"].sum()
         out = m(x)
         loss, _ = crit(out, {"images": x, "masks": masks}, 0)
         loss.backward()
