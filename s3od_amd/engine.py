@@ -431,6 +431,7 @@ class DPTEngine:
         Drop both, so the next call allocates fresh zeros and bumps only its own counters."""
         self._zpool = {}
         self._nbt = []
+        self._wg = DPTEngine._wg
 
     def forward(self, x, train=False, rope_rescale=None, ctx: Ctx | None = None):
         """x: [B,3,H,W] fp32 CUDA (normalised image).  Returns the reference output dict."""
@@ -506,14 +507,16 @@ class DPTEngine:
         dz2 = torch.empty_like(d_out)
         L("s3od_bn_bwd", self.dt, d_out, c["z2"], None, c["bn2"]["mean"], c["bn2"]["rstd"], P[q + "bn2.weight"], sums, dz2,
           G[q + "bn2.weight"], G[q + "bn2.bias"], G[q + "conv2.bias"], npix, 256, st)
-        self._wgrad_conv(dz2, c["a1"], B, h, w, 256, h, w, 256, 3, 1, 1, G[q + "conv2.weight"])
+        self._wg(lambda: self._wgrad_conv(dz2, c["a1"], B, h, w, 256, h, w, 256, 3, 1, 1, G[q + "conv2.weight"]),
+                 dz2, c["a1"])
         da1 = self._dgrad_conv(dz2, W8[tag + ".c2"], B, h, w, 256, h, w, 256, 3, 1, 1, wT=W8.get(tag + ".c2T"))
         dz1 = torch.empty_like(d_out)
         # ReLU mask recomputed from z1 and bn1's scale/shift (bit-identical to a1 > 0): a1 is not read
         L("s3od_bn_relu_bwd", self.dt, da1, c["z1"], c["bn1"]["scale"], c["bn1"]["shift"], c["bn1"]["mean"],
           c["bn1"]["rstd"], P[q + "bn1.weight"], sums, dz1,
           G[q + "bn1.weight"], G[q + "bn1.bias"], G[q + "conv1.bias"], npix, 256, st)
-        self._wgrad_conv(dz1, c["x"], B, h, w, 256, h, w, 256, 3, 1, 1, G[q + "conv1.weight"], relu_x=True)
+        self._wg(lambda: self._wgrad_conv(dz1, c["x"], B, h, w, 256, h, w, 256, 3, 1, 1, G[q + "conv1.weight"], relu_x=True),
+                 dz1, c["x"])
         return self._dgrad_conv_res(dz1, W8[tag + ".c1"], B, h, w, 256, ACT_RELU_BWD, c["x"], d_out, wT=W8.get(tag + ".c1T"))
 
     def _fusion_bwd(self, r, d_p, B, ctx, G, bcast=None, two_inputs=True):
@@ -527,7 +530,7 @@ class DPTEngine:
         q = f"seg_head.scratch.refinenet{r}."
         npix = B * h * w
         self._colsum(dc, npix, 256, G[q + "out_conv.bias"])
-        self._wgrad_lin(dc, c["s"], 256, 256, npix, G[q + "out_conv.weight"])
+        self._wg(lambda: self._wgrad_lin(dc, c["s"], 256, 256, npix, G[q + "out_conv.weight"]), dc, c["s"])
         ds2 = torch.empty_like(dc)
         self._dgrad_lin(dc, W8[f"ref{r}.out"], npix, 256, 256, ds2)
         ds = self._rcu_bwd(ds2, r, 2, B, ctx, G)
@@ -536,10 +539,33 @@ class DPTEngine:
         dx1 = self._rcu_bwd(ds, r, 1, B, ctx, G)
         return ds, dx1
 
+    _wg = staticmethod(lambda fn, *ts: fn())     # weight-gradient runner (decoder_backward installs the side-stream one)
+
     def decoder_backward(self, ctx, d_logits, d_iou, G, d_feat=None):
         lib().phase = "decoder"
         L, P, W8, dt = lib(), self.p, self.w, self.dt
         st = stream()
+        # weight gradients on the side stream (as in the encoder backward), concurrent with the data-gradient chain:
+        # the decoder's many small-map convs (64^2, 32^2 at bs 16: a fraction of a round of tiles) and the wgrads'
+        # tails then share the CUs.  Each wgrad only reads its operands; they are marked as used on the side stream
+        # (record_stream), so the caching allocator keeps them until it has run.  S3OD_DEC_SIDE=0 (or
+        # S3OD_BWD_SIDE=0): inline on the main stream.
+        main = torch.cuda.current_stream(d_logits.device)
+        side = (self._side_stream(d_logits.device) if os.environ.get("S3OD_BWD_SIDE", "1") != "0"
+                and os.environ.get("S3OD_DEC_SIDE", "1") != "0" else None)
+        self._dec_side = side
+
+        def wg(fn, *ts):
+            if side is None:
+                return fn()
+            e = torch.cuda.Event()
+            e.record(main)
+            side.wait_event(e)
+            with torch.cuda.stream(side):
+                fn()
+            for t in ts:
+                t.record_stream(side)
+        self._wg = wg
         B, ph, pw = ctx.B, ctx.ph, ctx.pw
         hd = ctx.t["head"]
         h = "seg_head."
@@ -554,19 +580,22 @@ class DPTEngine:
         dh = torch.empty((npx, 32 * nm), dtype=self.tdt, device=dev)
         L("s3od_mask_heads_bwd", dt, d_logits.contiguous(), hd["hsave"], W8["heads2"], dh, G["heads2_w"], G["heads2_b"],
           G["heads1_b"], B, HH * WW, nm, st)
-        self._wgrad_conv(dh, c64, B, HH, WW, 64, HH, WW, 32 * nm, 3, 1, 1, G["heads1_w"])
+        self._wg(lambda: self._wgrad_conv(dh, c64, B, HH, WW, 64, HH, WW, 32 * nm, 3, 1, 1, G["heads1_w"]), dh, c64)
         # (bias gradients are column sums fused into the epilogue that produces each gradient)
         d64 = self._dgrad_conv(dh, W8["heads1"], B, HH, WW, 64, HH, WW, 32 * nm, 3, 1, 1, act=ACT_RELU_BWD, res1=c64,
                                colsum=G[m + "upsample_2x.2.bias"], wT=W8.get("heads1T"))
         # ---- upsample_2x.2 conv 64->64 + ReLU
-        self._wgrad_conv(d64, up, B, HH, WW, 64, HH, WW, 64, 3, 1, 1, G[m + "upsample_2x.2.weight"])
+        self._wg(lambda: self._wgrad_conv(d64, up, B, HH, WW, 64, HH, WW, 64, 3, 1, 1, G[m + "upsample_2x.2.weight"]),
+                 d64, up)
         dup = self._dgrad_conv(d64, W8["c64"], B, HH, WW, 64, HH, WW, 64, 3, 1, 1, act=ACT_RELU_BWD, res1=up,
                                colsum=G[m + "upsample_2x.0.bias"], wT=W8.get("c64T"))
         # ---- upsample_2x.0 ConvTranspose 128->64 k4 s2 p1 + ReLU (conv view: Y=oc1 grid, X=up grid)
-        self._wgrad_conv(oc1, dup, B, HH, WW, 64, H1, W1, 128, 4, 2, 1, G[m + "upsample_2x.0.weight"])
+        self._wg(lambda: self._wgrad_conv(oc1, dup, B, HH, WW, 64, H1, W1, 128, 4, 2, 1, G[m + "upsample_2x.0.weight"]),
+                 oc1, dup)
         doc1 = self._conv(dup, W8["up2x"], B, HH, WW, 64, 128, 4, 2, 1, colsum=G[m + "output_conv1.bias"])
         # ---- output_conv1 3x3 256->128
-        self._wgrad_conv(doc1, p1, B, H1, W1, 256, H1, W1, 128, 3, 1, 1, G[m + "output_conv1.weight"])
+        self._wg(lambda: self._wgrad_conv(doc1, p1, B, H1, W1, 256, H1, W1, 128, 3, 1, 1, G[m + "output_conv1.weight"]),
+                 doc1, p1)
         dp1 = self._dgrad_conv(doc1, W8["oc1"], B, H1, W1, 256, H1, W1, 128, 3, 1, 1, wT=W8.get("oc1T"))
         if d_feat is not None:     # gradient of the returned features (= path_1, NCHW view)
             dp1.add_(d_feat.permute(0, 2, 3, 1).to(dp1.dtype))
@@ -589,25 +618,30 @@ class DPTEngine:
         for i, f in enumerate(feats):
             hh, ww = dims[i]
             C = f.shape[3]
-            self._wgrad_conv(drn[i], f, B, hh, ww, C, hh, ww, 256, 3, 1, 1, G[h + f"scratch.layer{i + 1}_rn.weight"])
+            self._wg(lambda: self._wgrad_conv(drn[i], f, B, hh, ww, C, hh, ww, 256, 3, 1, 1, G[h + f"scratch.layer{i + 1}_rn.weight"]),
+                     drn[i], f)
             dfeat.append(self._dgrad_conv(drn[i], W8[f"rn{i + 1}"], B, hh, ww, C, hh, ww, 256, 3, 1, 1, colsum=G[fbias[i]],
                                           wT=W8.get(f"rn{i + 1}T")))
         proj = dec["proj"]
         dproj = [None] * 4
         # resize0: ConvT 256 k4 s4 (conv view: Y = proj0 grid, X = f0 grid)
-        self._wgrad_conv(proj[0], dfeat[0], B, dims[0][0], dims[0][1], 256, ph, pw, 256, 4, 4, 0, G[h + "resize_layers.0.weight"])
+        self._wg(lambda: self._wgrad_conv(proj[0], dfeat[0], B, dims[0][0], dims[0][1], 256, ph, pw, 256, 4, 4, 0, G[h + "resize_layers.0.weight"]),
+                 proj[0], dfeat[0])
         dproj[0] = self._conv(dfeat[0], W8["rs0"], B, dims[0][0], dims[0][1], 256, 256, 4, 4, 0, colsum=G[h + "projects.0.bias"])
-        self._wgrad_conv(proj[1], dfeat[1], B, dims[1][0], dims[1][1], 512, ph, pw, 512, 2, 2, 0, G[h + "resize_layers.1.weight"])
+        self._wg(lambda: self._wgrad_conv(proj[1], dfeat[1], B, dims[1][0], dims[1][1], 512, ph, pw, 512, 2, 2, 0, G[h + "resize_layers.1.weight"]),
+                 proj[1], dfeat[1])
         dproj[1] = self._conv(dfeat[1], W8["rs1"], B, dims[1][0], dims[1][1], 512, 512, 2, 2, 0, colsum=G[h + "projects.1.bias"])
         dproj[2] = dfeat[2]
-        self._wgrad_conv(dfeat[3], proj[3], B, ph, pw, 1024, dims[3][0], dims[3][1], 1024, 3, 2, 1, G[h + "resize_layers.3.weight"])
+        self._wg(lambda: self._wgrad_conv(dfeat[3], proj[3], B, ph, pw, 1024, dims[3][0], dims[3][1], 1024, 3, 2, 1, G[h + "resize_layers.3.weight"]),
+                 dfeat[3], proj[3])
         dproj[3] = self._dgrad_conv(dfeat[3], W8["rs3"], B, ph, pw, 1024, dims[3][0], dims[3][1], 1024, 3, 2, 1,
                                     colsum=G[h + "projects.3.bias"])
         # projects (1x1, bias) -> tap gradients
         NP = ph * pw
         dtaps = []
         for i, c in enumerate(OUT_CH):
-            self._wgrad_lin(dproj[i], dec["taps"][i], c, self.D, B * NP, G[h + f"projects.{i}.weight"])
+            self._wg(lambda: self._wgrad_lin(dproj[i], dec["taps"][i], c, self.D, B * NP, G[h + f"projects.{i}.weight"]),
+                     dproj[i], dec["taps"][i])
             dtaps.append((dproj[i], c))
         lib().phase = None
         return dtaps
@@ -741,8 +775,17 @@ class DPTEngine:
         gradient of the returned ``features`` (NCHW), added to path_1's."""
         try:
             dtaps = self.decoder_backward(ctx, d_logits, d_iou, G, d_feat=d_feat)
+            self._wg = DPTEngine._wg
             if self.grad_hook is not None:
-                self.grad_hook("seg_head")
+                side = self._dec_side
+                if side is None:
+                    self.grad_hook("seg_head")
+                else:     # the decoder's gradients are final once both streams are past it: hook from the side stream
+                    e = torch.cuda.Event()
+                    e.record(torch.cuda.current_stream(d_logits.device))
+                    side.wait_event(e)
+                    with torch.cuda.stream(side):
+                        self.grad_hook("seg_head")
             self.encoder_backward(ctx, dtaps, G)
         except BaseException:
             self._invalidate()

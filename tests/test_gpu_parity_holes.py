@@ -39,7 +39,7 @@ def test_fused_adamw_matches_torch():
         oa.step(); ob.step()
     torch.cuda.synchronize()
     for pa, pb in zip(a, b):
-        assert float((pa - pb).abs().max() / pb.abs().max()) <= 1e-6
+        assert float((pa - pb).detach().abs().max() / pb.detach().abs().max()) <= 1e-6
         for key in ("exp_avg", "exp_avg_sq"):
             sa, sb = oa.state[pa][key], ob.state[pb][key]
             assert float((sa - sb).abs().max() / sb.abs().max()) <= 1e-6, key
