@@ -1234,48 +1234,106 @@ static float* slab_scratch(hipStream_t st, size_t bytes) {
 // S3OD_WGRAD_SLAB=0 (read per call): the fp32-atomic split-K epilogue instead of the slabs (A/B)
 static bool slab_ok() { return !getenv_zero("S3OD_WGRAD_SLAB"); }
 
-// M-tail launches (split_tail: the <= 255 rows past the last full 256-row panel, on 128x128 tiles): a tail has only
-// N/128 tiles (6 for N 768), each a full-K main loop on an otherwise idle chip (35-45 us at K 3072).  Split-K instead:
-// sp K ranges write fp32 slabs [sp][M][N] (EpiWgradPart), then tail_epi_kernel sums them per 16 x 128 tile in LDS and
-// runs the op's own epilogue functor on the sum (bias / scale / act / residuals / pre / column sums, unchanged).
-// S3OD_TAIL_SK=0 (read per call): the single full-K tail launch.
-template <class EPI>
-__global__ void __launch_bounds__(256) tail_epi_kernel(const float* __restrict__ ws, int sp, int M, int N, EPI epi) {
-  constexpr int TM = 16, TN = 128, LDT = TN + 4;
-  __shared__ __attribute__((aligned(16))) float ct[TM * LDT];     // also the column-sum reduction's 256 x 8 floats
-  const int tid = threadIdx.x, m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
-  const int r = tid >> 4, c = (tid & 15) * 8;
-  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (m0 + r < M && n0 + c < N) {
-    const float* p = ws + (long)(m0 + r) * N + n0 + c;
-    for (int z = 0; z < sp; z++, p += (long)M * N) {
-      const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
-      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+// M-tail launches (split_tail: the <= 255 rows past the last full 256-row panel).  On 128x128 tiles a tail has only
+// N/128 workgroups (6 for N 768), each a full-K main loop on an otherwise idle chip (13-45 us at K 768-3072).  bf16:
+// a skinny full-K kernel instead -- one wave per 16 x 16 output block (240 waves for 80 x 768), operands straight from
+// global memory (80 rows of A and the B panel stay in L2), and the SAME v_mfma_f32_16x16x32_bf16 chain over K, in the
+// same order and fragment layout as the ping-pong / 128x128 kernels (lane (g, l) holds row l, k = 32 kk + 8 g .. +7,
+// zero past K), so every tail row is bit-identical to what a full panel computes: outputs do not depend on where a
+// row falls, i.e. on the batch size.  (A split-K tail was as fast but broke that: bf16 bs-8 vs bs-1 rel-L2 1e-2.)
+// Block = 4 waves = 16 rows x 64 columns; the fp32 tile is staged in LDS and the op's own epilogue functor runs on it.
+template <bool BKC, class EPI>
+__global__ void __launch_bounds__(256) tail_gemm_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ Bp,
+                                                        long ldb, int M, int N, int K, EPI epi) {
+  constexpr int LDT = 64 + 4;
+  __shared__ __attribute__((aligned(16))) float ct[2048];     // 16 x 68 C tile; the column-sum reduction reads 256 x 8
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, l = lane & 15;
+  const int m0 = blockIdx.y * 16, nb0 = blockIdx.x * 64, am = m0 + l, bn = nb0 + wave * 16 + l;
+  const bool aok = am < M, bok = bn < N;
+  // rows past M / columns past N read row 0 / column 0 instead (clamped addresses, no branches in the loop): an
+  // output element only sees its own A row and B column, and those rows / columns are never stored
+  const bf16* ar = A + (long)(aok ? am : 0) * lda;
+  const long bo = bok ? bn : 0;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  // N-contiguous B (dgrad: w [K][N]): a fragment wants 8 k of one column, so the wave stages each k-step's 32 x 16
+  // block through LDS -- lane j fetches 16 B of row k = j / 2 (columns 8 (j & 1) ..), the fragment is read back as 8
+  // bf16 of column l (row stride 24 elements = 48 B: 16-B aligned stores; no bank conflicts on the reads)
+  constexpr int U = 16, RS = 24;                           // U = 32: 283 VGPRs, spills
+  __shared__ bf16 bst[BKC ? 1 : 4 * U * 32 * RS];
+  bf16* wst = bst + (BKC ? 0 : wave * U * 32 * RS);
+  const int bj = lane >> 1, bc = 8 * (lane & 1);
+  const long bcol = (nb0 + wave * 16 + bc < N) ? nb0 + wave * 16 + bc : 0;   // whole 16-B chunks: N % 8 == 0
+  auto load = [&](int k, bf16x8& fa, bf16x8& fb) {            // K % 8 == 0: a lane's 8 k are all in range or all out
+    fa = *(const bf16x8*)(ar + k);
+    if constexpr (BKC) fb = *(const bf16x8*)(Bp + bo * ldb + k);
+  };
+  // a lone wave's chain is load-latency bound: the loads of U k-steps are issued together, then their U MFMAs run
+  // in k order ((B, A) operand order, as Mma<bf16> in the kernels)
+  const int KF = K / 32;
+  int kk = 0;
+  for (; kk + U <= KF; kk += U) {
+    bf16x8 fa[U], fb[U];
+    uint4 braw[BKC ? 1 : U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      load((kk + u) * 32 + 8 * g, fa[u], fb[u]);
+      if constexpr (!BKC) braw[u] = *(const uint4*)(Bp + (long)((kk + u) * 32 + bj) * ldb + bcol);
     }
+    if constexpr (!BKC) {
+#pragma unroll
+      for (int u = 0; u < U; u++) *(uint4*)(wst + (u * 32 + bj) * RS + bc) = braw[u];
+#pragma unroll
+      for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int e = 0; e < 8; e++) fb[u][e] = wst[(u * 32 + 8 * g + e) * RS + l];
+    }
+    __builtin_amdgcn_sched_barrier(0);                        // all U loads in flight before the first MFMA waits
+#pragma unroll
+    for (int u = 0; u < U; u++) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[u], fa[u], acc, 0, 0, 0);
   }
-  *(float4*)(ct + r * LDT + c) = make_float4(v[0], v[1], v[2], v[3]);
-  *(float4*)(ct + r * LDT + c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  for (; kk < KF; kk++) {
+    bf16x8 fa, fb;
+    load(kk * 32 + 8 * g, fa, fb);
+    if constexpr (!BKC) {
+#pragma unroll
+      for (int e = 0; e < 8; e++) fb[e] = Bp[(long)(kk * 32 + 8 * g + e) * ldb + bo];
+    }
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa, acc, 0, 0, 0);
+  }
+  if (K % 32) {                                               // K tail: lanes past K contribute zeros
+    bf16x8 fa, fb;
+    const int k = KF * 32 + 8 * g;
+    if (k < K) {
+      load(k, fa, fb);
+      if constexpr (!BKC) {
+#pragma unroll
+        for (int e = 0; e < 8; e++) fb[e] = Bp[(long)(k + e) * ldb + bo];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; e++) { fa[e] = (bf16)0.f; fb[e] = (bf16)0.f; }
+    }
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa, acc, 0, 0, 0);
+  }
+  *(f32x4*)(ct + l * LDT + wave * 16 + 4 * g) = acc;          // lane (g, l) owns C[m0 + l][n + 4g .. 4g+3]
   __syncthreads();
   epi.prepare(0);
-  epi(ct, LDT, m0, n0, tid, TM, TN, 256);
+  epi(ct, LDT, m0, nb0, tid, 16, 64, 256);
 }
-template <typename T, int BM, int BN, int NST, int WM, class LA, class LB, class EPI>
-static int launch_tail(LA la, LB lb, EPI e, int M, int N, int KTILES, hipStream_t st) {
-  const int tiles = cdiv(M, BM) * cdiv(N, BN), sp = std::min(256 / tiles, KTILES / 4);
-  float* ws = (sp >= 2 && M < 256 && N % 8 == 0 && !getenv_zero("S3OD_TAIL_SK")) ? slab_scratch(st, (size_t)sp * M * N * 4)
-                                                                               : nullptr;
-  if (!ws) return launch_igemm<T, BM, BN, LA, LB, EPI, NST, WM>(la, lb, e, M, N, KTILES, 1, 1, st);
-  EpiWgradPart part{ws, M, N};
-  int rc = launch_igemm<T, BM, BN, LA, LB, EpiWgradPart, NST, WM>(la, lb, part, M, N, KTILES, sp, 1, st);
-  if (rc) return rc;
-  hipLaunchKernelGGL(tail_epi_kernel<EPI>, dim3(cdiv(N, 128), cdiv(M, 16)), dim3(256), 0, st, ws, sp, M, N, e);
-  return s3od_check_launch("igemm tail epilogue");
+template <class LA, class LB, class EPI>
+static int launch_tail_gemm(const LA& la, const LB& lb, EPI e, int M, int N, hipStream_t st) {
+  hipLaunchKernelGGL((tail_gemm_kernel<LB::KCL, EPI>), dim3(cdiv(N, 64), cdiv(M, 16)), dim3(256), 0, st,
+                     (const bf16*)la.p, la.ld, (const bf16*)lb.p, lb.ld, M, N, la.K, e);
+  return s3od_check_launch("igemm tail");
 }
-// the launch of one with_cfg config: the M-tail form (split-K) when this is a tail launch on 128x128 tiles
+// the launch of one with_cfg config: the skinny tail kernel for a bf16 M-tail launch (tl_cfg == 1, A K-contiguous, no
+// ReLU-on-load); f32 tails stay on the 128x128 kernel (same summation order too).  S3OD_TAIL_SKINNY=0 (read per call):
+// the 128x128 tail launch in bf16 as well.
 template <typename T, class C, class LA, class LB, class EPI>
 static int launch_op(LA la, LB lb, EPI e, int M, int N, int KTILES, hipStream_t st) {
-  if constexpr (!C::PP)
-    if (tl_cfg == 1) return launch_tail<T, C::BM, C::BN, C::NST, C::WM>(la, lb, e, M, N, KTILES, st);
+  if constexpr (!C::PP && sizeof(T) == 2 && LA::KCL)
+    if (tl_cfg == 1 && M < 256 && !la.relu && !lb.relu && !getenv_zero("S3OD_TAIL_SKINNY"))
+      return launch_tail_gemm(la, lb, e, M, N, st);
   return launch_igemm<T, C::BM, C::BN, LA, LB, EPI, C::NST, C::WM>(la, lb, e, M, N, KTILES, 1, 1, st);
 }
 

@@ -225,33 +225,36 @@ def test_pp_production_rows_65616():
     assert rel_l2(dw, dw0 + dh.float().t() @ x.float()) < 1e-5
 
 
-@pytest.mark.parametrize("tail_sk", ["1", "0"])
-def test_pp_tail_split_k_epilogues(tail_sk, monkeypatch):
-    """The M-tail launch as split-K (fp32 slabs summed by tail_epi_kernel, which then runs the op's own epilogue) and
-    as the single full-K launch (S3OD_TAIL_SK=0): GELU'-multiplied dgrad with the column sums the engine uses for bias
-    gradients (fp32 atomics), the o_proj form (bias, LayerScale, fp32 residual, pre) and QKV + RoPE, each over
-    65536 + 80 rows (K 3072 / 768), checked on the tail rows and the column sums against fp32 torch."""
-    monkeypatch.setenv("S3OD_TAIL_SK", tail_sk)
+def test_pp_tail_kernel_bit_identical(monkeypatch):
+    """The M-tail launch on the skinny full-K kernel (tail_gemm_kernel: one wave per 16 x 16 block, operands from
+    global memory) must equal the 128x128 tail launch (S3OD_TAIL_SKINNY=0) BIT FOR BIT -- same MFMA chain over K,
+    same fragment layout -- which is what keeps outputs independent of the batch size (a row's position relative to
+    the 256-row panels).  Forms: GELU'-multiplied dgrad with the bias column sums (B operand N-contiguous), the
+    down-projection forward (bias, LayerScale, fp32 residual, pre; B K-contiguous), each over 65536 + 80 rows, plus
+    the fp32-torch check of the tail rows."""
     torch.manual_seed(80)
     L, s = _lib()
     M, D, F = 65536 + 80, 768, 3072
-    # down-projection dgrad: dx = (dy w) * g (ACT_MUL, g = saved gelu'), colsum += sum_m dx
     dy, w, g = r(M, D), r(D, F, scale=D ** -0.5), r(M, F)
-    dx = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
-    cs = torch.zeros(F, device="cuda")
-    L("s3od_linear_dgrad", BF16, M, F, D, dy, D, w, 6, g, F, dx, F, 0, 0, 0, 0, cs, s)
-    ref = (dy.float() @ w.float()) * g.float()
-    torch.cuda.synchronize()
-    assert rel_l2(dx[-80:].float(), ref[-80:]) < 4e-3 and rel_l2(dx.float(), ref) < 4e-3
-    assert rel_l2(cs, ref.sum(0)) < 1e-4          # the column sums are of the fp32 values, before the bf16 store
-    del dy, w, g, dx, ref
-    # o_proj forward: out_f32 = (x w^T + b) * ls + res, pre stored; K 3072 (down-projection shape)
-    x, w, b, ls = r(M, F), r(D, F, scale=F ** -0.5), r(D, dt=torch.float32), r(D, dt=torch.float32)
+    x, w2, b, ls = r(M, F), r(D, F, scale=F ** -0.5), r(D, dt=torch.float32), r(D, dt=torch.float32)
     res = r(M, D, dt=torch.float32)
-    out = torch.empty(M, D, device="cuda")
-    pre = torch.empty(M, D, device="cuda", dtype=torch.bfloat16)
-    L("s3od_linear_fwd", BF16, M, D, F, x, F, w, b, ls, None, 0, res, D, None, 0, 1, out, D, 1, pre, D, 0, 0, 0, s)
-    p = x.float() @ w.float().t() + b
-    torch.cuda.synchronize()
-    assert rel_l2(out[-80:], p[-80:] * ls + res[-80:]) < 1e-5
-    assert rel_l2(pre[-80:].float(), p[-80:]) < 4e-3
+    outs = {}
+    for knob in ("1", "0"):
+        monkeypatch.setenv("S3OD_TAIL_SKINNY", knob)
+        dx = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
+        cs = torch.zeros(F, device="cuda")
+        L("s3od_linear_dgrad", BF16, M, F, D, dy, D, w, 6, g, F, dx, F, 0, 0, 0, 0, cs, s)
+        out = torch.empty(M, D, device="cuda")
+        pre = torch.empty(M, D, device="cuda", dtype=torch.bfloat16)
+        L("s3od_linear_fwd", BF16, M, D, F, x, F, w2, b, ls, None, 0, res, D, None, 0, 1, out, D, 1, pre, D, 0, 0, 0, s)
+        torch.cuda.synchronize()
+        outs[knob] = (dx[-80:].clone(), cs, out[-80:].clone(), pre[-80:].clone())
+        del dx, out, pre
+    for a, c in zip(outs["1"][:1] + outs["1"][2:], outs["0"][:1] + outs["0"][2:]):
+        assert torch.equal(a, c)
+    assert rel_l2(outs["1"][1], outs["0"][1]) < 1e-5       # column sums: fp32 atomics, order may differ
+    ref = (dy[-80:].float() @ w.float()) * g[-80:].float()
+    assert rel_l2(outs["1"][0].float(), ref) < 4e-3
+    p = x[-80:].float() @ w2.float().t() + b
+    assert rel_l2(outs["1"][2], p * ls + res[-80:]) < 1e-5
+    assert rel_l2(outs["1"][3].float(), p) < 4e-3

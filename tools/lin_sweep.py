@@ -129,7 +129,8 @@ if __name__ == "__main__":
     if os.environ.get("SWEEP") == "tail":
         # cost of the 80-row M tail: the fwd / dgrad shapes at 65536 rows (whole panels), 65616 (+ tail launch) and
         # the tail alone (80 rows; S3OD_GEMM_CFG selects its config)
-        for m in (65536, 65616, 80, 65536, 65616, 80):
+        ms = [int(v) for v in os.environ.get("TAIL_MS", "65536,65616,80").split(",")] * 2
+        for m in ms:
             M = m
             print(f"--- M={m}", flush=True)
             fwd("o_proj fwd N768 K768 (res f32, out f32, pre)", D, D, res_f32=True, out_f32=True, pre=True, scale=True)
