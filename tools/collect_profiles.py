@@ -65,7 +65,10 @@ tot = sum(float(r["TotalDurationNs"]) for r in rows)
 lines = [f"# rocprofv3 kernel stats, round tag {tag}", "",
          "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline "
          "--no-infer --no-breakdown` (configs[2]: bf16, bs 16, 1024², training step)",
-         f"Total kernel time {tot / 1e6:.1f} ms over {steps} steps = {tot / 1e6 / steps:.1f} ms/step.", "",
+         f"Total kernel time {tot / 1e6:.1f} ms over {steps} steps = {tot / 1e6 / steps:.1f} ms/step.",
+         "The backward's weight gradients run on a side stream beside the data-gradient chain (encoder since r04a, "
+         "decoder since r04b), so kernels of the two streams overlap: each duration includes the CU sharing, and the "
+         "sum exceeds the step's wall time (the bench line's ms_per_step).", "",
          "| ms/step | % | calls | avg us | kernel |", "|---:|---:|---:|---:|---|"]
 for r in rows[:45]:
     lines.append(f"| {float(r['TotalDurationNs']) / 1e6 / steps:.2f} | {float(r['Percentage']):.2f} | {r['Calls']} | "
