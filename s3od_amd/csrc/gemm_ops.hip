@@ -13,6 +13,7 @@
 static RowMap dense_rm() { RowMap r{}; r.mode = 0; return r; }
 // a per-call dev switch: true when the variable is set to 0 (A/B inside one process)
 static bool getenv_zero(const char* n) { const char* e = getenv(n); return e && atoi(e) == 0; }
+static int getenv_int(const char* n) { const char* e = getenv(n); return e ? atoi(e) : -1; }
 
 // Tile configuration (dev knob for the micro-benchmarks): S3OD_GEMM_CFG=<n> forces one config for
 // every GEMM entry point; default (-1) = per-op choice below.
@@ -1506,16 +1507,18 @@ int s3od_qkv_rope_fwd(int dtype, int B, int Ntok, int P, int H, const void* x, c
 }
 
 // the 3x3 s1 p1 convs whose output channels fill 256-wide tiles and whose pixel tiles fill whole rounds of the
-// chip run on the ping-pong kernel (S3OD_CONV_PP=0, read per call, keeps the 128x128 implicit GEMM: A/B runs)
 // chip run on the ping-pong kernel when there are >= 8 rounds of tiles or K >= 9 * 512 (measured, tools/conv_cfg_bench.py,
 // bs 16: 256^2 RCU 1.38 vs 1.51-1.66 ms with BN sums, plain 1.21 vs 1.34-1.38 ms; 128^2 512 -> 256 0.56 vs 0.69-0.81 ms;
-// the 128^2 256 -> 256 RCU 0.39 vs 0.37-0.38 ms stays on 128x128 tiles)
-static bool conv_pp_ok(const ConvGeo& g, int M, int N) {
+// the 128^2 256 -> 256 RCU 0.39 vs 0.37-0.38 ms with BN sums stays on 128x128 tiles), and from 4 rounds without BN
+// statistics (eval: the C5 256^2 bs-4 RCUs, C5 74.72 -> 74.47 ms, C2 24.99 -> 24.91 ms per batch; train +0.07 %, noise,
+// profiles/r04b_conv_pp_rounds_ab.txt).  S3OD_CONV_PP=0 (read per call): the 128x128 implicit GEMM (A/B runs);
+// S3OD_CONV_PP=2: from 4 rounds with BN statistics too.
+static bool conv_pp_ok(const ConvGeo& g, int M, int N, bool stats) {
   const int nch = g.SC / 64;
   const long tiles = (long)(M / 256) * (N / 256);
+  const bool rounds = tiles >= 2048 || g.SC >= 512 || (tiles >= 1024 && (!stats || getenv_int("S3OD_CONV_PP") == 2));
   return tl_cfg < 0 && gemm_cfg() < 0 && g.KH == 3 && g.KW == 3 && g.s == 1 && g.p == 1 && g.RH == g.SH && g.RW == g.SW &&
-         g.SC % 64 == 0 && (nch & (nch - 1)) == 0 && N % 256 == 0 && pp_pays(M, N) && (tiles >= 2048 || g.SC >= 512) &&
-         !getenv_zero("S3OD_CONV_PP");
+         g.SC % 64 == 0 && (nch & (nch - 1)) == 0 && N % 256 == 0 && pp_pays(M, N) && rounds && !getenv_zero("S3OD_CONV_PP");
 }
 
 // implicit-GEMM conv forward (im2col gathered per K tile by ConvFwdA); also the stride-1 3x3 data gradient run as a
@@ -1527,7 +1530,7 @@ static int conv_fwd_igemm(int dtype, ConvGeo g, int M, int N, int K, int Cin, in
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(K, KT<T>::BK);
     if constexpr (sizeof(T) == 2) {
-      if (conv_pp_ok(g, M, N)) {
+      if (conv_pp_ok(g, M, N, stats != nullptr)) {
         // 3x3 s1 p1 with 256-multiple output channels: the 256x256 ping-pong kernel (one workgroup per CU covers
         // all 256 output channels of 256 pixels, so each im2col A tile is gathered once) with the Conv3A loader
         auto pp = [&](auto rl) -> int {
