@@ -276,7 +276,9 @@ def test_bf16_vs_oracle_production_sizes(model):
         top2 = torch.topk(ref["pred_iou"][0], 2).values
         rec[tag] = {"batch": B, "size": S, "logits_rel_l2": rel_l2(pm, r), "max_abs_diff": maxd,
                     "median_abs_logit": float(r.abs().median()), "flip_band_fraction": float(band.float().mean()),
-                    "sign_agreement": float(agree.float().mean()), "sign_agreement_outside_band": float(agree[~band].float().mean()),
+                    "sign_agreement": float(agree.double().mean()),
+                    "sign_agreement_outside_band": float(agree[~band].double().mean()),
+                    "sign_flips_outside_band": int((~agree & ~band).sum()),
                     "mask_iou": inter / max(union, 1.0), "pred_iou_rel_l2": rel_l2(iou, ref["pred_iou"]),
                     "best_idx": int(iou.argmax(1)), "best_idx_ref": int(ref["pred_iou"].argmax(1)),
                     "ref_top2_margin": float(top2[0] - top2[1])}
@@ -302,7 +304,7 @@ def test_bf16_vs_oracle_production_sizes(model):
     for tag in ("C2", "C5"):
         r = rec[tag]
         assert r["logits_rel_l2"] <= 3e-2 and r["sign_agreement"] >= 0.98, (tag, r)
-        assert r["sign_agreement_outside_band"] == 1.0, (tag, r)
+        assert r["sign_flips_outside_band"] == 0, (tag, r)     # counted exactly (a float32 mean over 16M pixels is not)
         assert r["pred_iou_rel_l2"] <= 3e-2, (tag, r)
         if r["ref_top2_margin"] > 0.05:
             assert r["best_idx"] == r["best_idx_ref"], (tag, r)

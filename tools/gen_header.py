@@ -15,7 +15,6 @@ REF = {
     "s3od_linear_dgrad": "autograd of nn.Linear w.r.t. input (reference: implicit torch autograd)",
     "s3od_linear_wgrad": "autograd of nn.Linear w.r.t. weight (reference: implicit torch autograd)",
     "s3od_qkv_rope_fwd": "DINOv3ViTAttention q/k/v_proj + apply_rotary_pos_emb: tf:modeling_dinov3_vit.py:294-314, 238-268",
-    "s3od_ln_qkv_rope_fwd": "DINOv3ViTLayer norm1 -> q/k/v_proj + RoPE fused (measurement prototype, not on the engine path): tf:modeling_dinov3_vit.py:419-445, 294-314",
     "s3od_conv_fwd": "nn.Conv2d forward (3x3 s1/s2, 1x1) + BatchNorm/ReLU/residual: src/s3od/model.py:144-159, 244-345, 437-452",
     "s3od_conv_dgrad": "nn.ConvTranspose2d forward (src/s3od/model.py:146-153, 437-439) and Conv2d input-gradient",
     "s3od_conv_wgrad": "Conv2d / ConvTranspose2d weight gradient (reference: implicit torch autograd)",
