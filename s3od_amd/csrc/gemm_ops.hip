@@ -1509,14 +1509,16 @@ int s3od_qkv_rope_fwd(int dtype, int B, int Ntok, int P, int H, const void* x, c
 // the 3x3 s1 p1 convs whose output channels fill 256-wide tiles and whose pixel tiles fill whole rounds of the
 // chip run on the ping-pong kernel when there are >= 8 rounds of tiles or K >= 9 * 512 (measured, tools/conv_cfg_bench.py,
 // bs 16: 256^2 RCU 1.38 vs 1.51-1.66 ms with BN sums, plain 1.21 vs 1.34-1.38 ms; 128^2 512 -> 256 0.56 vs 0.69-0.81 ms;
-// the 128^2 256 -> 256 RCU 0.39 vs 0.37-0.38 ms with BN sums stays on 128x128 tiles), and from 4 rounds without BN
-// statistics (eval: the C5 256^2 bs-4 RCUs, C5 74.72 -> 74.47 ms, C2 24.99 -> 24.91 ms per batch; train +0.07 %, noise,
-// profiles/r04b_conv_pp_rounds_ab.txt).  S3OD_CONV_PP=0 (read per call): the 128x128 implicit GEMM (A/B runs);
-// S3OD_CONV_PP=2: from 4 rounds with BN statistics too.
+// the 128^2 256 -> 256 RCU 0.39 vs 0.37-0.38 ms with BN sums stays on 128x128 tiles), and from 2 rounds without BN
+// statistics (eval: 4 rounds = the C5 256^2 bs-4 RCUs, C5 74.72 -> 74.47 ms, C2 24.99 -> 24.91 ms per batch; 2 rounds =
+// the C2 128^2 bs-8 RCUs, C2 25.37 -> 25.25 ms; 1 round mixed; profiles/r04b_conv_pp_rounds_ab.txt).
+// S3OD_CONV_PP=0 (read per call): the 128x128 implicit GEMM (A/B runs); S3OD_CONV_PP=2: the eval threshold with BN
+// statistics too; S3OD_CONV_PP_MIN: the eval threshold in 256x256 tiles (default 512).
 static bool conv_pp_ok(const ConvGeo& g, int M, int N, bool stats) {
   const int nch = g.SC / 64;
   const long tiles = (long)(M / 256) * (N / 256);
-  const bool rounds = tiles >= 2048 || g.SC >= 512 || (tiles >= 1024 && (!stats || getenv_int("S3OD_CONV_PP") == 2));
+  const int min_ns = getenv_int("S3OD_CONV_PP_MIN") > 0 ? getenv_int("S3OD_CONV_PP_MIN") : 512;    // (A/B, per call)
+  const bool rounds = tiles >= 2048 || g.SC >= 512 || (tiles >= min_ns && (!stats || getenv_int("S3OD_CONV_PP") == 2));
   return tl_cfg < 0 && gemm_cfg() < 0 && g.KH == 3 && g.KW == 3 && g.s == 1 && g.p == 1 && g.RH == g.SH && g.RW == g.SW &&
          g.SC % 64 == 0 && (nch & (nch - 1)) == 0 && N % 256 == 0 && pp_pays(M, N) && rounds && !getenv_zero("S3OD_CONV_PP");
 }
