@@ -1243,7 +1243,7 @@ static bool slab_ok() { return !getenv_zero("S3OD_WGRAD_SLAB"); }
 // zero past K), so every tail row is bit-identical to what a full panel computes: outputs do not depend on where a
 // row falls, i.e. on the batch size.  (A split-K tail was as fast but broke that: bf16 bs-8 vs bs-1 rel-L2 1e-2.)
 // Block = 4 waves = 16 rows x 64 columns; the fp32 tile is staged in LDS and the op's own epilogue functor runs on it.
-template <bool BKC, class EPI>
+template <bool BKC, int U, class EPI>
 __global__ void __launch_bounds__(256) tail_gemm_kernel(const bf16* __restrict__ A, long lda, const bf16* __restrict__ Bp,
                                                         long ldb, int M, int N, int K, EPI epi) {
   constexpr int LDT = 64 + 4;
@@ -1259,7 +1259,7 @@ __global__ void __launch_bounds__(256) tail_gemm_kernel(const bf16* __restrict__
   // N-contiguous B (dgrad: w [K][N]): a fragment wants 8 k of one column, so the wave stages each k-step's 32 x 16
   // block through LDS -- lane j fetches 16 B of row k = j / 2 (columns 8 (j & 1) ..), the fragment is read back as 8
   // bf16 of column l (row stride 24 elements = 48 B: 16-B aligned stores; no bank conflicts on the reads)
-  constexpr int U = 16, RS = 24;                           // U = 32: 283 VGPRs, spills
+  constexpr int RS = 24;
   __shared__ bf16 bst[BKC ? 1 : 4 * U * 32 * RS];
   bf16* wst = bst + (BKC ? 0 : wave * U * 32 * RS);
   const int bj = lane >> 1, bc = 8 * (lane & 1);
@@ -1323,9 +1323,23 @@ __global__ void __launch_bounds__(256) tail_gemm_kernel(const bf16* __restrict__
 }
 template <class LA, class LB, class EPI>
 static int launch_tail_gemm(const LA& la, const LB& lb, EPI e, int M, int N, hipStream_t st) {
-  hipLaunchKernelGGL((tail_gemm_kernel<LB::KCL, EPI>), dim3(cdiv(N, 64), cdiv(M, 16)), dim3(256), 0, st,
-                     (const bf16*)la.p, la.ld, (const bf16*)lb.p, lb.ld, M, N, la.K, e);
-  return s3od_check_launch("igemm tail");
+  // U = k-steps whose loads are in flight together: the largest that divides K / 32 (a remainder runs one step at a
+  // time, each paying the full latency).  K-contiguous B: up to 24 (U = 32: 283 VGPRs, spills); N-contiguous B (LDS
+  // staging, 4 U KB per wave): up to 16.
+  const int KF = la.K / 32;
+  auto go = [&](auto u) {
+    hipLaunchKernelGGL((tail_gemm_kernel<LB::KCL, decltype(u)::value, EPI>), dim3(cdiv(N, 64), cdiv(M, 16)), dim3(256), 0, st,
+                       (const bf16*)la.p, la.ld, (const bf16*)lb.p, lb.ld, M, N, la.K, e);
+    return s3od_check_launch("igemm tail");
+  };
+  if constexpr (LB::KCL) {
+    if (KF % 24 == 0) return go(std::integral_constant<int, 24>{});
+    if (KF % 16 == 0) return go(std::integral_constant<int, 16>{});
+  } else {
+    if (KF % 16 == 0) return go(std::integral_constant<int, 16>{});
+    if (KF % 12 == 0) return go(std::integral_constant<int, 12>{});
+  }
+  return go(std::integral_constant<int, 8>{});
 }
 // the launch of one with_cfg config: the skinny tail kernel for a bf16 M-tail launch (tl_cfg == 1, A K-contiguous, no
 // ReLU-on-load); f32 tails stay on the 128x128 kernel (same summation order too).  S3OD_TAIL_SKINNY=0 (read per call):
