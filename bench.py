@@ -514,8 +514,10 @@ def main():
                                rccl_version=".".join(map(str, torch.cuda.nccl.version())) if hasattr(torch.cuda, "nccl") else None,
                                channels={k: os.environ[k] for k in ("NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS") if k in os.environ}
                                or "RCCL default (NCCL_MIN/MAX_NCHANNELS unset)",
-                               note="HIP events: per-bucket all-reduce on the comm stream; comm_exposed_ms = the compute "
-                                    "stream's wait from backward end to GradSync.finish()'s join, per step")
+                               note="HIP events. buckets[].ms: bucket start on the comm stream -> the collective's end "
+                                    "(event recorded behind Work.wait() on the comm stream); allreduce_ms_per_step: union of "
+                                    "the step's bucket intervals; bus_GBps: 2(N-1)/N x bytes / that union; comm_exposed_ms: "
+                                    "the compute stream's wait from backward end to GradSync.finish()'s join, per step")
         if bd is not None:
             res["breakdown"] = bd
         if args.mode == "train" and world == 1 and not args.no_infer and args.dtype == "bf16":

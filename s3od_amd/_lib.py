@@ -29,6 +29,14 @@ _CT = {
 _DECL = re.compile(r"^(int|const char\*)\s+(s3od_\w+)\(([^)]*)\);", re.M)
 
 
+def parse_nrep(path=HEADER):
+    """S3OD_NREP: replicas of the accumulation workspaces (their sizes are stated in the header)."""
+    return int(re.search(r"#define S3OD_NREP (\d+)", Path(path).read_text()).group(1))
+
+
+NREP = parse_nrep()
+
+
 def parse_header(path=HEADER):
     decls = {}
     for ret, name, args in _DECL.findall(Path(path).read_text()):

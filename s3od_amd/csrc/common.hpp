@@ -106,17 +106,39 @@ DEV float gelu_fast_grad(float x) {
   return 0.5f * (1.0f + f) + x * (0.39894228040143268f * e);
 }
 
-// integer dev knob read once from the environment (micro-benchmark sweeps only; default otherwise)
+// Dispatch / dev knobs (A/B switches and micro-benchmark sweeps; the defaults are the product path).
+// S3OD_KNOB(name, def) reads the environment ONCE, on the first call through that site, into a function-local
+// static; the per-call path never calls getenv.  S3OD_AB=1 (itself read once) re-reads every knob on every call,
+// for the tests and tools that toggle a knob between calls inside one process (A/B of two kernels).
 #include <stdlib.h>
 static inline int dev_knob(const char* name, int def) {
   const char* e = getenv(name);
   return e ? atoi(e) : def;
 }
+static inline bool s3od_ab_mode() {
+  static const bool ab = dev_knob("S3OD_AB", 0) != 0;
+  return ab;
+}
+#define S3OD_KNOB(name, def) \
+  (s3od_ab_mode() ? dev_knob(name, def) : [] { static const int v_ = dev_knob(name, def); return v_; }())
+// true when the knob is set to 0 (the "off" switch of a specialised path)
+#define S3OD_OFF(name) (S3OD_KNOB(name, 1) == 0)
 
 // Column reductions over many workgroups add into S3OD_NREP replicas of the accumulator
 // (workgroup b -> replica b % S3OD_NREP) and a second pass folds the replicas: fp32/fp64 atomics
 // from ~1000 workgroups onto the same few KB serialise at the memory side (measured 2-3x slower
 // end to end for the BN backward / q,v-bias reductions).
 constexpr int S3OD_NREP = 32;
+
+// compute units of the current device (read once per process)
+static inline int s3od_cu_count() {
+  static const int n = [] {
+    int dev = 0, c = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    return c > 0 ? c : 256;
+  }();
+  return n;
+}
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

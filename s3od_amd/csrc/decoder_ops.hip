@@ -599,7 +599,7 @@ static int bn_bwd_impl(int dtype, const void* dy, const void* z, const void* y_r
   // blocks per pass (tools/hbm_bench.py bn, bs 16 x 256 channels): 1024 for >= 256K pixels (1M: 606 -> 542 us,
   // 256K: 173 -> 150 us), 512 below (64K: 1024 blocks of 64 pixels pay more in atomics: 61 -> 82 us)
   const int rows = 256 / (C / 8);
-  static const int nb_knob = dev_knob("S3OD_BN_BLOCKS", 0);
+  const int nb_knob = S3OD_KNOB("S3OD_BN_BLOCKS", 0);
   long ppb = max(64L, npix / (nb_knob > 0 ? nb_knob : (npix >= 262144 ? 1024 : 512)));
   ppb = (ppb + rows - 1) / rows * rows;
   const int nb = cdiv(npix, ppb);

@@ -1242,9 +1242,9 @@ static int launch_igemm(LA la, LB lb, EPI epi, int M, int N, int KTILES, int spl
       return 22;
     }
     auto kfn = igemm_pp_kernel<LA, LB, EPI>;
-    static bool attr = false;
-    if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS); attr = true; }
-    static const int flags = dev_knob("S3OD_PP_FLAGS", 0);
+    static const bool attr = ((void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS), true);   // once per process (thread-safe static init)
+    (void)attr;
+    const int flags = S3OD_KNOB("S3OD_PP_FLAGS", 0);
     dim3 grid(cdiv(N, BN), cdiv(M, BM), split * zdim_extra);
     hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), PP_LDS, st, la, lb, epi, KTILES, split, flags);
     return s3od_check_launch("igemm_pp");
@@ -1255,8 +1255,8 @@ static int launch_igemm(LA la, LB lb, EPI epi, int M, int N, int KTILES, int spl
     }
     typedef GemmShape<T, BM, BN, NST, WM_> S;
     auto kfn = igemm_kernel<T, BM, BN, NST, LA, LB, EPI, WM_>;
-    static bool attr = false;
-    if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS); attr = true; }
+    static const bool attr = ((void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS), true);   // once per process (thread-safe static init)
+    (void)attr;
     dim3 grid(cdiv(N, BN), cdiv(M, BM), split * zdim_extra);
     hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), S::LDS, st, la, lb, epi, KTILES, split);
     return s3od_check_launch("igemm");

@@ -11,9 +11,6 @@
   } while (0)
 
 static RowMap dense_rm() { RowMap r{}; r.mode = 0; return r; }
-// a per-call dev switch: true when the variable is set to 0 (A/B inside one process)
-static bool getenv_zero(const char* n) { const char* e = getenv(n); return e && atoi(e) == 0; }
-static int getenv_int(const char* n) { const char* e = getenv(n); return e ? atoi(e) : -1; }
 
 // Tile configuration (dev knob for the micro-benchmarks): S3OD_GEMM_CFG=<n> forces one config for
 // every GEMM entry point; default (-1) = per-op choice below.
@@ -21,11 +18,7 @@ static int getenv_int(const char* n) { const char* e = getenv(n); return e ? ato
 //   3: 256x128, 2 stages (BN is clamped to 64 for 64-channel convs: 256x64 x 2 stages = 80 KB)
 //   4: 256x256, 2 stages (1 WG/CU, per-wave 64x128; C staged in two 128-row halves)
 #include <stdlib.h>
-static int gemm_cfg() {
-  static int c = -2;
-  if (c == -2) { const char* e = getenv("S3OD_GEMM_CFG"); c = e ? atoi(e) : -1; }
-  return c;
-}
+static int gemm_cfg() { return S3OD_KNOB("S3OD_GEMM_CFG", -1); }
 // W = waves that issue the operand loads (the loaders are built for that many waves)
 // PP_: the 256x256 ping-pong kernel (bf16 only), whose loaders stage half tiles (LM / LN rows)
 template <int BM_, int BN_, int NST_, int W_ = GEMM_WAVES, int WM_ = 0, bool PP_ = false> struct TileCfg {
@@ -47,7 +40,7 @@ struct TailCfg {
 // extra round of full-K tiles (e.g. o_proj 3078 tiles on 512 slots = 7 rounds, 6 without the tail);
 // they run as a second, small launch on 128x128 tiles instead.  Dev knob S3OD_M_TAIL=0 disables.
 static bool split_tail(int M) {
-  static const int knob = dev_knob("S3OD_M_TAIL", 1);
+  const int knob = S3OD_KNOB("S3OD_M_TAIL", 1);
   return knob && tl_cfg < 0 && M > 256 && (M & 255) != 0;
 }
 // the 256x256 ping-pong kernel (one workgroup per CU) only pays when its tiles fill whole rounds of
@@ -462,10 +455,9 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
   wait_vmcnt<0>();        // no LDS-DMA (dummy pieces included) may still be landing when the workgroup retires
 }
 
-// S3OD_CONV_RW=0 disables the path (read per call: an A/B inside one process)
+// S3OD_CONV_RW=0 disables the path (an A/B inside one process under S3OD_AB=1)
 static bool rw_ok(int dtype, int B, int H, int W) {
-  const char* e = getenv("S3OD_CONV_RW");
-  return dtype == S3OD_BF16 && !(e && atoi(e) == 0) && (long)H * W * 192 < (1L << 31) && B > 0;
+  return dtype == S3OD_BF16 && !S3OD_OFF("S3OD_CONV_RW") && (long)H * W * 192 < (1L << 31) && B > 0;
 }
 template <int MODE, int CI>
 static int launch_rw(const bf16* x, const bf16* w, const float* bias, const bf16* res1, float* colsum, bf16* out,
@@ -473,14 +465,12 @@ static int launch_rw(const bf16* x, const bf16* w, const float* bias, const bf16
                      float* logits = nullptr) {
   typedef RwShape<CI> S;
   auto kfn = conv3x3_c64_rw_kernel<MODE, CI>;
-  static bool attr = false;
-  if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS); attr = true; }
+  static const bool attr = ((void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS), true);   // once per process (thread-safe static init)
+  (void)attr;
   const int tx = cdiv(W, S::TW), ty = cdiv(H, S::TH);
   const long tiles = (long)B * tx * ty;
   if (tiles >= (1L << 31)) { s3od_set_error("conv rw: too many tiles"); return 22; }
-  static int ncu = 0;
-  if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
-  const int nwg = (int)std::min<long>(std::max<long>(tiles, 8), (long)ncu);   // one persistent WG per CU, >= 8 so every XCD owns its range
+    const int nwg = (int)std::min<long>(std::max<long>(tiles, 8), (long)s3od_cu_count());   // one persistent WG per CU, >= 8 so every XCD owns its range
   hipLaunchKernelGGL(kfn, dim3(nwg), dim3(256), S::LDS, st, x, w, bias, res1, colsum, out, H, W, tx, ty, (int)tiles, w2, b2,
                      logits);
   return s3od_check_launch("conv3x3_c64_rw");
@@ -770,34 +760,32 @@ __global__ void __launch_bounds__(256, 1) conv4s2_rw_kernel(const bf16* __restri
 }
 static int launch_conv4s2_rw(const bf16* x, const bf16* w, float* colsum, bf16* out, int B, int H, int W, hipStream_t st) {
   auto kfn = conv4s2_rw_kernel;
-  static bool attr = false;
-  if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, cs2::LDS); attr = true; }
+  static const bool attr = ((void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, cs2::LDS), true);   // once per process (thread-safe static init)
+  (void)attr;
   const int tx = cdiv(W, cs2::TW), ty = cdiv(H, cs2::TH);
   const long tiles = (long)B * tx * ty;
   if (tiles >= (1L << 31)) { s3od_set_error("conv s2 rw: too many tiles"); return 22; }
-  static int ncu = 0;
-  if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
-  const int nwg = (int)std::min<long>(std::max<long>(tiles, 8), (long)ncu);
+    const int nwg = (int)std::min<long>(std::max<long>(tiles, 8), (long)s3od_cu_count());
   hipLaunchKernelGGL(kfn, dim3(nwg), dim3(256), cs2::LDS, st, x, w, colsum, out, H, W, tx, ty, (int)tiles);
   return s3od_check_launch("conv4s2_rw");
 }
 
-// S3OD_CONVT_RW=0 disables the path (read per call)
+// S3OD_CONVT_RW=0 disables the path (under S3OD_AB=1: per call)
 static bool convt_rw_ok(int dtype, int B, int H, int W) {
-  const char* e = getenv("S3OD_CONVT_RW");
-  return dtype == S3OD_BF16 && !(e && atoi(e) == 0) && B > 0 && (long)4 * H * W * 128 < (1L << 31);
+  return dtype == S3OD_BF16 && !S3OD_OFF("S3OD_CONVT_RW") && B > 0 && (long)4 * H * W * 128 < (1L << 31);
 }
 static int launch_convt_rw(const bf16* x, const bf16* wt, const float* bias, bool relu, bf16* out, int B, int H, int W,
                            hipStream_t st) {
   auto kfn = relu ? convT4s2_rw_kernel<true> : convT4s2_rw_kernel<false>;
-  static bool attr[2] = {false, false};
-  if (!attr[relu]) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, ct::LDS); attr[relu] = true; }
+  static const bool attr0 = ((void)hipFuncSetAttribute((const void*)convT4s2_rw_kernel<false>,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, ct::LDS), true);
+  static const bool attr1 = ((void)hipFuncSetAttribute((const void*)convT4s2_rw_kernel<true>,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, ct::LDS), true);
+  (void)attr0; (void)attr1;
   const int tx = cdiv(W, ct::TW), ty = cdiv(H, ct::TH);
   const long tiles = (long)B * tx * ty;
   if (tiles >= (1L << 31)) { s3od_set_error("convT rw: too many tiles"); return 22; }
-  static int ncu = 0;
-  if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
-  const int nwg = (int)std::min<long>(std::max<long>(tiles, 8), (long)ncu);   // >= 8: every XCD owns a tile range
+    const int nwg = (int)std::min<long>(std::max<long>(tiles, 8), (long)s3od_cu_count());   // >= 8: every XCD owns a tile range
   hipLaunchKernelGGL(kfn, dim3(nwg), dim3(256), ct::LDS, st, x, wt, bias, out, H, W, tx, ty, (int)tiles);
   return s3od_check_launch("convT4s2_rw");
 }
@@ -923,15 +911,13 @@ template <int CO, bool RELU>
 static int launch_wgrad_halo(const bf16* dy, const bf16* x, float* ws, int B, int H, int W, int CinT, int CoT, hipStream_t st) {
   typedef WgShape<CO> S;
   auto kfn = conv3x3_wgrad_halo_kernel<CO, RELU>;
-  static bool attr = false;
-  if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS); attr = true; }
+  static const bool attr = ((void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS), true);   // once per process (thread-safe static init)
+  (void)attr;
   const int tx = cdiv(W, HT_TW), ty = cdiv(H, HT_TH);
   const long tiles = (long)B * tx * ty;
-  static int ncu = 0;
-  if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
-  // one persistent workgroup per CU (registers) over all channel blocks: each block gets ~ncu/blocks of them
+    // one persistent workgroup per CU (registers) over all channel blocks: each block gets ~ncu/blocks of them
   const int nci = CinT / 64, nblk = (CoT / CO) * nci;
-  const int wpc = (int)std::max<long>(1, std::min<long>(tiles, std::max(1, ncu / nblk)));
+  const int wpc = (int)std::max<long>(1, std::min<long>(tiles, std::max(1, s3od_cu_count() / nblk)));
   hipLaunchKernelGGL(kfn, dim3(nblk * wpc), dim3(S::NT), S::LDS, st, dy, x, ws, H, W, tx, ty, (int)tiles, CinT, CoT, nci, wpc);
   return s3od_check_launch("conv3x3_wgrad_halo");
 }
@@ -1133,31 +1119,27 @@ conv4s2_wgrad_dma_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x
 }
 static int launch_wgrad4s2(const bf16* dy, const bf16* x, float* ws, int B, int OH, int OW, int CinT, int CoT, hipStream_t st) {
   auto kfn = conv4s2_wgrad_dma_kernel;
-  static bool attr = false;
-  if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, wg4::LDS); attr = true; }
+  static const bool attr = ((void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, wg4::LDS), true);   // once per process (thread-safe static init)
+  (void)attr;
   const int tx = cdiv(OW, wg4::TW), ty = cdiv(OH, wg4::TH);
   const long tiles = (long)B * tx * ty;
   if (tiles >= (1L << 31)) { s3od_set_error("wgrad 4s2: too many tiles"); return 22; }
-  static int ncu = 0;
-  if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
-  const int nci = CinT / 64, nblk = (CoT / 64) * nci;
-  const int wpc = (int)std::max<long>(1, std::min<long>(tiles, std::max(1, ncu / nblk)));
+    const int nci = CinT / 64, nblk = (CoT / 64) * nci;
+  const int wpc = (int)std::max<long>(1, std::min<long>(tiles, std::max(1, s3od_cu_count() / nblk)));
   hipLaunchKernelGGL(kfn, dim3(nblk * wpc), dim3(256), wg4::LDS, st, dy, x, ws, OH, OW, tx, ty, (int)tiles, CinT, CoT, nci, wpc);
   return s3od_check_launch("conv4s2_wgrad_dma");
 }
 
-// S3OD_WGRAD_DMA=0 (read per call) keeps the register-staged kernel
+// S3OD_WGRAD_DMA=0 (under S3OD_AB=1: per call) keeps the register-staged kernel
 template <bool RELU>
 static int launch_wgrad_dma(const bf16* dy, const bf16* x, float* ws, int B, int H, int W, int CinT, int CoT, hipStream_t st) {
   auto kfn = conv3x3_wgrad_dma_kernel<RELU>;
-  static bool attr = false;
-  if (!attr) { (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, wgd::LDS); attr = true; }
+  static const bool attr = ((void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, wgd::LDS), true);   // once per process (thread-safe static init)
+  (void)attr;
   const int tx = cdiv(W, HT_TW), ty = cdiv(H, HT_TH);
   const long tiles = (long)B * tx * ty;
-  static int ncu = 0;
-  if (!ncu) { int dev = 0; (void)hipGetDevice(&dev); (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev); if (ncu <= 0) ncu = 256; }
-  const int nci = CinT / 64, nblk = (CoT / 64) * nci;
-  const int wpc = (int)std::max<long>(1, std::min<long>(tiles, std::max(1, ncu / nblk)));
+    const int nci = CinT / 64, nblk = (CoT / 64) * nci;
+  const int wpc = (int)std::max<long>(1, std::min<long>(tiles, std::max(1, s3od_cu_count() / nblk)));
   hipLaunchKernelGGL(kfn, dim3(nblk * wpc), dim3(256), wgd::LDS, st, dy, x, ws, H, W, tx, ty, (int)tiles, CinT, CoT, nci, wpc);
   return s3od_check_launch("conv3x3_wgrad_dma");
 }
@@ -1208,32 +1190,8 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int sp, int M,
   }
 }
 
-// per-stream scratch for the split-K slabs (grown on demand, kept for the process; calls on one stream run in order,
-// so a stream's slab is free again once its reduce kernel has run)
-static float* slab_scratch(hipStream_t st, size_t bytes) {
-  struct Ent { hipStream_t st; float* p; size_t n; };
-  static Ent tab[8] = {};
-  for (auto& e : tab) {
-    if (e.p && e.st == st) {
-      if (e.n >= bytes) return e.p;
-      (void)hipStreamSynchronize(st);
-      (void)hipFree(e.p);
-      e.p = nullptr;
-      if (hipMalloc((void**)&e.p, bytes) != hipSuccess) { e.p = nullptr; return nullptr; }
-      e.n = bytes;
-      return e.p;
-    }
-  }
-  for (auto& e : tab)
-    if (!e.p) {
-      if (hipMalloc((void**)&e.p, bytes) != hipSuccess) return nullptr;
-      e.st = st; e.n = bytes;
-      return e.p;
-    }
-  return nullptr;
-}
-// S3OD_WGRAD_SLAB=0 (read per call): the fp32-atomic split-K epilogue instead of the slabs (A/B)
-static bool slab_ok() { return !getenv_zero("S3OD_WGRAD_SLAB"); }
+// S3OD_WGRAD_SLAB=0 (under S3OD_AB=1: per call): the fp32-atomic split-K epilogue instead of the slabs (A/B)
+static bool slab_ok() { return !S3OD_OFF("S3OD_WGRAD_SLAB"); }
 
 // M-tail launches (split_tail: the <= 255 rows past the last full 256-row panel).  On 128x128 tiles a tail has only
 // N/128 workgroups (6 for N 768), each a full-K main loop on an otherwise idle chip (13-45 us at K 768-3072).  bf16:
@@ -1260,6 +1218,7 @@ __global__ void __launch_bounds__(256) tail_gemm_kernel(const bf16* __restrict__
   // block through LDS -- lane j fetches 16 B of row k = j / 2 (columns 8 (j & 1) ..), the fragment is read back as 8
   // bf16 of column l (row stride 24 elements = 48 B: 16-B aligned stores; no bank conflicts on the reads)
   constexpr int RS = 24;
+  static_assert(sizeof(float) * 2048 + (BKC ? 2 : 2 * 4 * U * 32 * RS) <= 160 * 1024, "tail_gemm: LDS budget (gfx950: 160 KiB)");
   __shared__ bf16 bst[BKC ? 1 : 4 * U * 32 * RS];
   bf16* wst = bst + (BKC ? 0 : wave * U * 32 * RS);
   const int bj = lane >> 1, bc = 8 * (lane & 1);
@@ -1281,8 +1240,15 @@ __global__ void __launch_bounds__(256) tail_gemm_kernel(const bf16* __restrict__
       if constexpr (!BKC) braw[u] = *(const uint4*)(Bp + (long)((kk + u) * 32 + bj) * ldb + bcol);
     }
     if constexpr (!BKC) {
+      // the wave's LDS block is written and read back by different lanes of the same wave: order the previous
+      // batch's reads before these stores and these stores before the reads (wave-scope fence + wave barrier: the
+      // C++ model does not order cross-lane LDS traffic within a wave by itself)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int u = 0; u < U; u++) *(uint4*)(wst + (u * 32 + bj) * RS + bc) = braw[u];
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int u = 0; u < U; u++)
 #pragma unroll
@@ -1342,12 +1308,12 @@ static int launch_tail_gemm(const LA& la, const LB& lb, EPI e, int M, int N, hip
   return go(std::integral_constant<int, 8>{});
 }
 // the launch of one with_cfg config: the skinny tail kernel for a bf16 M-tail launch (tl_cfg == 1, A K-contiguous, no
-// ReLU-on-load); f32 tails stay on the 128x128 kernel (same summation order too).  S3OD_TAIL_SKINNY=0 (read per call):
+// ReLU-on-load); f32 tails stay on the 128x128 kernel (same summation order too).  S3OD_TAIL_SKINNY=0 (under S3OD_AB=1: per call):
 // the 128x128 tail launch in bf16 as well.
 template <typename T, class C, class LA, class LB, class EPI>
 static int launch_op(LA la, LB lb, EPI e, int M, int N, int KTILES, hipStream_t st) {
   if constexpr (!C::PP && sizeof(T) == 2 && LA::KCL)
-    if (tl_cfg == 1 && M < 256 && !la.relu && !lb.relu && !getenv_zero("S3OD_TAIL_SKINNY"))
+    if (tl_cfg == 1 && M < 256 && !la.relu && !lb.relu && !S3OD_OFF("S3OD_TAIL_SKINNY"))
       return launch_tail_gemm(la, lb, e, M, N, st);
   return launch_igemm<T, C::BM, C::BN, LA, LB, EPI, C::NST, C::WM>(la, lb, e, M, N, KTILES, 1, 1, st);
 }
@@ -1408,7 +1374,7 @@ int s3od_linear_fwd(int dtype, int M, int N, int K, const void* x, long ldx, con
         DenseKC<T, decltype(C)::LN, decltype(C)::W> lb{(const T*)w, (long)K, N, K, 0};
         EpiStd<TO, TR, T> e{(TO*)out, ldo, 0, bias, scale, shift, (const TR*)res1, ldr1, (const TR*)res2, ldr2,
                             (T*)pre, ldp, nullptr, act, M, N, rm};
-        static const int epi_probe = dev_knob("S3OD_EPI_PROBE", 0);   // dev: 1 = skip the epilogue's stores
+        const int epi_probe = S3OD_KNOB("S3OD_EPI_PROBE", 0);   // dev: 1 = skip the epilogue's stores
         if (epi_probe == 1) e.M = 0;
         return launch_op<T, decltype(C)>(la, lb, e, M, N, KTILES, st);
       });
@@ -1460,11 +1426,36 @@ int s3od_linear_dgrad(int dtype, int M, int N, int K, const void* dy, long lddy,
   return 0;
 }
 
-// dw[n_out, k_in] += sum_rows dy[row, n_out] x[row, k_in]   (fp32 atomics, split over rows)
+// split-K slab floats a linear weight gradient uses (0: the fp32-atomic epilogue, no slab): the ping-pong kernel's
+// split-K partials go to sp caller-owned fp32 slabs [sp][Nout][Kin], summed by wgrad_reduce_kernel
+static long linear_wgrad_slab_floats(int dtype, int Nout, int Kin, int rows, int split) {
+  if (dtype != S3OD_BF16 || !slab_ok() || Kin % 4 != 0) return 0;
+  const int KTILES = cdiv(rows, KT<bf16>::BK);
+  const int def = (long)Nout * Kin <= 1024L * 1024 ? 0 : 5;
+  return with_cfg<bf16>(def, [&](auto C) -> long {
+    if constexpr (!decltype(C)::PP) return 0;
+    else {
+      const int sp = split > 0 ? split : wgrad_split<bf16, 256, 256, 2>(cdiv(Nout, 256) * cdiv(Kin, 256), KTILES);
+      return sp > 1 ? (long)sp * Nout * Kin : 0;
+    }
+  });
+}
+
+// bytes of the slab workspace s3od_linear_wgrad uses for these arguments (0 = none needed)
+int s3od_linear_wgrad_ws(int dtype, int Nout, int Kin, int rows, int split, long* bytes) {
+  S3OD_REQUIRE(bytes != nullptr, "linear_wgrad_ws: null output");
+  *bytes = 4 * linear_wgrad_slab_floats(dtype, Nout, Kin, rows, split);
+  return 0;
+}
+
+// dw[n_out, k_in] += sum_rows dy[row, n_out] x[row, k_in]  (split over rows: fp32 atomics into dw, or -- when the
+// caller passes a slab of >= s3od_linear_wgrad_ws bytes -- per-split fp32 slabs summed into dw by a second kernel)
 int s3od_linear_wgrad(int dtype, int Nout, int Kin, int rows, const void* dy, long lddy,
-                      const void* x, long ldx, float* dw, int split, void* stream) {
+                      const void* x, long ldx, float* dw, int split, float* slab, long slab_bytes, void* stream) {
   S3OD_REQUIRE(Nout % 8 == 0 && Kin % 8 == 0, "linear_wgrad: dims %% 8");
   hipStream_t st = (hipStream_t)stream;
+  const long need = slab ? linear_wgrad_slab_floats(dtype, Nout, Kin, rows, split) : 0;
+  if (need == 0 || slab_bytes < 4 * need) slab = nullptr;
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(rows, KT<T>::BK);
     // measured (tools/lin_sweep.py, bs16 1024^2 ViT shapes): the 256x256 ping-pong kernel for the large
@@ -1476,7 +1467,6 @@ int s3od_linear_wgrad(int dtype, int Nout, int Kin, int rows, const void* dy, lo
       DenseMC<T, decltype(C)::LM, decltype(C)::W> la{(const T*)dy, lddy, rows, Nout};
       DenseMC<T, decltype(C)::LN, decltype(C)::W> lb{(const T*)x, ldx, rows, Kin};
       if constexpr (decltype(C)::PP) {
-        float* slab = (slab_ok() && sp > 1 && Kin % 4 == 0) ? slab_scratch(st, (size_t)sp * Nout * Kin * 4) : nullptr;
         if (slab) {
           EpiWgradPart e{slab, Nout, Kin};
           int rc = launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, Nout, Kin, KTILES, sp, 1, st);
@@ -1486,7 +1476,7 @@ int s3od_linear_wgrad(int dtype, int Nout, int Kin, int rows, const void* dy, lo
         }
       }
       EpiWgrad e{dw, Nout, Kin, Kin, 1};
-      static const int epi_probe = dev_knob("S3OD_EPI_PROBE", 0);   // dev: 1 = skip the split-K atomics (timing only)
+      const int epi_probe = S3OD_KNOB("S3OD_EPI_PROBE", 0);   // dev: 1 = skip the split-K atomics (timing only)
       if (epi_probe == 1) e.M = 0;
       return launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, Nout, Kin, KTILES, sp, 1, st);
     });
@@ -1526,15 +1516,15 @@ int s3od_qkv_rope_fwd(int dtype, int B, int Ntok, int P, int H, const void* x, c
 // the 128^2 256 -> 256 RCU 0.39 vs 0.37-0.38 ms with BN sums stays on 128x128 tiles), and from 2 rounds without BN
 // statistics (eval: 4 rounds = the C5 256^2 bs-4 RCUs, C5 74.72 -> 74.47 ms, C2 24.99 -> 24.91 ms per batch; 2 rounds =
 // the C2 128^2 bs-8 RCUs, C2 25.37 -> 25.25 ms; 1 round mixed; profiles/r04b_conv_pp_rounds_ab.txt).
-// S3OD_CONV_PP=0 (read per call): the 128x128 implicit GEMM (A/B runs); S3OD_CONV_PP=2: the eval threshold with BN
+// S3OD_CONV_PP=0 (under S3OD_AB=1: per call): the 128x128 implicit GEMM (A/B runs); S3OD_CONV_PP=2: the eval threshold with BN
 // statistics too; S3OD_CONV_PP_MIN: the eval threshold in 256x256 tiles (default 512).
 static bool conv_pp_ok(const ConvGeo& g, int M, int N, bool stats) {
   const int nch = g.SC / 64;
   const long tiles = (long)(M / 256) * (N / 256);
-  const int min_ns = getenv_int("S3OD_CONV_PP_MIN") > 0 ? getenv_int("S3OD_CONV_PP_MIN") : 512;    // (A/B, per call)
-  const bool rounds = tiles >= 2048 || g.SC >= 512 || (tiles >= min_ns && (!stats || getenv_int("S3OD_CONV_PP") == 2));
+  const int min_ns = S3OD_KNOB("S3OD_CONV_PP_MIN", 512) > 0 ? S3OD_KNOB("S3OD_CONV_PP_MIN", 512) : 512;
+  const bool rounds = tiles >= 2048 || g.SC >= 512 || (tiles >= min_ns && (!stats || S3OD_KNOB("S3OD_CONV_PP", -1) == 2));
   return tl_cfg < 0 && gemm_cfg() < 0 && g.KH == 3 && g.KW == 3 && g.s == 1 && g.p == 1 && g.RH == g.SH && g.RW == g.SW &&
-         g.SC % 64 == 0 && (nch & (nch - 1)) == 0 && N % 256 == 0 && pp_pays(M, N) && rounds && !getenv_zero("S3OD_CONV_PP");
+         g.SC % 64 == 0 && (nch & (nch - 1)) == 0 && N % 256 == 0 && pp_pays(M, N) && rounds && !S3OD_OFF("S3OD_CONV_PP");
 }
 
 // implicit-GEMM conv forward (im2col gathered per K tile by ConvFwdA); also the stride-1 3x3 data gradient run as a
@@ -1633,7 +1623,7 @@ int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
                       : launch_rw<1, 96>((const bf16*)dy, (const bf16*)wT, nullptr, (const bf16*)res1, colsum, (bf16*)dx, B, H,
                                          W, (hipStream_t)stream);
   if (wT && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && (Cin != 64 || Cout > 96) && !pre &&
-      !stats && !getenv_zero("S3OD_DGRAD_WT")) {
+      !stats && !S3OD_OFF("S3OD_DGRAD_WT")) {
     // stride-1 3x3 data gradient = forward conv of dy (Cout channels) with wT [Cin][3][3][Cout]: the forward
     // gather (ConvFwdA) instead of the transposed-conv gather (measured faster on the 256-channel RCU convs)
     ConvGeo gf{}; gf.B = B; gf.SH = H; gf.SW = W; gf.SC = Cout; gf.RH = H; gf.RW = W; gf.KH = 3; gf.KW = 3; gf.s = 1; gf.p = 1;
@@ -1671,23 +1661,46 @@ int s3od_conv_dgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
   return 0;
 }
 
+// the 256-channel 3x3 s1 weight gradients on the ping-pong kernel (Wgrad3B): the split-K factor, 0 when the
+// call does not take that path
+static int conv_wgrad_pp_split(int dtype, int B, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW, int stride,
+                               int pad, int split) {
+  if (!(dtype == S3OD_BF16 && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && W % 64 == 0 &&
+        Cin % 256 == 0 && Cout % 256 == 0 && ((long)H * W >= 128L * 128 || Cin >= 512) && tl_cfg < 0 && gemm_cfg() < 0 &&
+        !S3OD_OFF("S3OD_WGRAD_PP")))
+    return 0;
+  const int KTILES = B * OH * OW / 64, tiles = (Cout / 256) * (9 * Cin / 256);
+  return split > 0 ? split : std::max(1, std::min(256 / tiles, KTILES / 8));
+}
+
+// bytes of the slab workspace s3od_conv_wgrad uses for these arguments (0 = none needed)
+int s3od_conv_wgrad_ws(int dtype, int B, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW, int stride,
+                       int pad, int split, long* bytes) {
+  S3OD_REQUIRE(bytes != nullptr, "conv_wgrad_ws: null output");
+  const int sp = slab_ok() ? conv_wgrad_pp_split(dtype, B, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad, split) : 0;
+  *bytes = sp > 1 ? 4L * sp * Cout * KH * KW * Cin : 0;
+  return 0;
+}
+
 // conv wgrad: dw[Cout][Cin][KH][KW] (PyTorch layout, fp32) += sum_pix dy[pix][co] * x[src(pix,tap)][ci]
 // dy: [B,OH,OW,Cout]; x: [B,H,W,Cin].  Also serves ConvTranspose2d weights (conv view).
 // ws (nullable): Cout*KH*KW*Cin floats, all zero on entry and left all zero (split-K partials in the GEMM layout)
+// slab (nullable): caller-owned scratch of slab_bytes (>= s3od_conv_wgrad_ws) for the ping-pong kernel's split-K slabs;
+// without it that path adds its partials into ws by fp32 atomics.  The library never allocates.
 int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW,
                     int stride, int pad, const void* dy, const void* x, int relu_x, float* dw, float* ws, int split,
-                    void* stream) {
+                    float* slab, long slab_bytes, void* stream) {
   S3OD_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "conv_wgrad: channels %% 8");
   ConvGeo g{}; g.B = B; g.SH = H; g.SW = W; g.SC = Cin; g.RH = OH; g.RW = OW; g.KH = KH; g.KW = KW; g.s = stride; g.p = pad;
   const int NPIX = B * OH * OW, M = Cout, N = KH * KW * Cin;
   hipStream_t st = (hipStream_t)stream;
-  static const int wg_knob = dev_knob("S3OD_WGRAD_HALO", 1);
+  const int wg_knob = S3OD_KNOB("S3OD_WGRAD_HALO", 1);
   // halo-tile kernel: 3x3 s1 p1, Cin a multiple of 64, Cout a multiple of 64 (or 96 for the mask heads).
   // Measured at bs 16 (tools/lin_sweep.py SWEEP=conv64): 2.4x / 1.75x on the 1024^2 64 -> 64 / 96 convs,
   // 1.2x on 512^2 256 -> 128, equal at 256^2 / 128^2 and 8 % slower at 64^2 -> used for Cin 64 or >= 512^2 maps
   if (dtype == S3OD_BF16 && ws && KH == 4 && KW == 4 && stride == 2 && pad == 1 && H == 2 * OH && W == 2 * OW && Cin % 64 == 0 &&
       Cout % 64 == 0 && !relu_x && (long)H * W * Cin * 2 < (1L << 31) && (long)OH * OW * Cout * 2 < (1L << 31) &&
-      !getenv_zero("S3OD_WGRAD_DMA")) {
+      !S3OD_OFF("S3OD_WGRAD_DMA")) {
     // the ConvTranspose2d(128, 64, 4, 2, 1) weight (upsample_2x.0) in its conv view
     int rc = launch_wgrad4s2((const bf16*)dy, (const bf16*)x, ws, B, OH, OW, Cin, Cout, st);
     if (rc) return rc;
@@ -1697,7 +1710,7 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
   const int coblk = Cout % 64 == 0 ? 64 : (Cout == 96 ? 96 : 0);
   if (wg_knob && dtype == S3OD_BF16 && ws && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W &&
       Cin % 64 == 0 && coblk && (Cin == 64 || (long)H * W >= 512L * 512)) {
-    const bool dma = coblk == 64 && (long)H * W * (Cin > Cout ? Cin : Cout) * 2 < (1L << 31) && !getenv_zero("S3OD_WGRAD_DMA");
+    const bool dma = coblk == 64 && (long)H * W * (Cin > Cout ? Cin : Cout) * 2 < (1L << 31) && !S3OD_OFF("S3OD_WGRAD_DMA");
     int rc = dma ? (relu_x ? launch_wgrad_dma<true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)
                            : launch_wgrad_dma<false>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)) :
              coblk == 64 ? (relu_x ? launch_wgrad_halo<64, true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)
@@ -1708,18 +1721,16 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
     hipLaunchKernelGGL(wgrad_permute_add_kernel, dim3(cdiv((long)M * N, 256)), dim3(256), 0, st, ws, dw, M, Cin, KH * KW);
     return s3od_check_launch("conv_wgrad permute");
   }
-  if (dtype == S3OD_BF16 && ws && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && W % 64 == 0 &&
-      Cin % 256 == 0 && Cout % 256 == 0 && ((long)H * W >= 128L * 128 || Cin >= 512) && tl_cfg < 0 && gemm_cfg() < 0 &&
-      !getenv_zero("S3OD_WGRAD_PP")) {
+  if (ws && conv_wgrad_pp_split(dtype, B, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad, split) > 0) {
     // the 256-channel RCU / layerK_rn weight gradients on the ping-pong kernel: one 256 x 256 tile = 256 output
     // channels x one tap's 256 input channels, K = pixels split over ~one round of workgroups (fp32 atomics into the
     // GEMM-layout workspace, then the permute into dW).  Measured vs the 128x128 implicit GEMM (tools/conv_cfg_bench.py
     // WG=1, bs 16): 256^2 1.47 vs 1.63-1.66 ms (ReLU'd input 1.52 vs 1.77-1.97), 128^2 0.39 vs 0.42, 128^2 512 -> 256
     // 0.76 vs 0.85, 64^2 1024 -> 256 0.38 vs 0.44; the 64^2 256 -> 256 one (0.14 vs 0.13 ms) stays on 128x128
-    const int KTILES = NPIX / 64, tiles = (Cout / 256) * (N / 256);
-    int sp = split > 0 ? split : std::max(1, std::min(256 / tiles, KTILES / 8));
+    const int KTILES = NPIX / 64;
+    const int sp = conv_wgrad_pp_split(dtype, B, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad, split);
     DenseMC<bf16, 128> la{(const bf16*)dy, (long)Cout, NPIX, Cout};
-    float* slab = (slab_ok() && sp > 1) ? slab_scratch(st, (size_t)sp * M * N * 4) : nullptr;
+    if (!(slab_ok() && sp > 1 && slab_bytes >= 4L * sp * M * N)) slab = nullptr;
     auto pp = [&](auto rl, auto e) -> int {
       Wgrad3B<128, decltype(rl)::value> lb{}; lb.x = (const bf16*)x; lb.B = B; lb.H = H; lb.W = W; lb.Cin = Cin;
       return launch_igemm<bf16, 256, 256, decltype(la), decltype(lb), decltype(e)>(la, lb, e, M, N, KTILES, sp, 1, st);

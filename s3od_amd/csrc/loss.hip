@@ -338,8 +338,8 @@ int s3od_mask_loss_bwd(const float* logits, const float* target, const float* co
   hipLaunchKernelGGL(loss_grad_kernel, dim3(cdiv(HW, 256), B * M), dim3(256), 0, st, logits, target, coef, iou_ws, gscale, dlogits,
                      M, HW, alpha, gamma);
   if (with_ssim) {
-    static bool attr = false;
-    if (!attr) { (void)hipFuncSetAttribute((const void*)ssim_grad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, SSIM_GRAD_LDS); attr = true; }
+    static const bool attr = ((void)hipFuncSetAttribute((const void*)ssim_grad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, SSIM_GRAD_LDS), true);   // once per process (thread-safe static init)
+    (void)attr;
     const int H = (int)(HW / W);
     hipLaunchKernelGGL(ssim_grad_kernel, dim3(cdiv(W, ST), cdiv(H, ST), B * M), dim3(256), SSIM_GRAD_LDS, st, logits, target, coef,
                        gscale, dlogits, M, H, W, gauss11());

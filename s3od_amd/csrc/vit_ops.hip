@@ -435,7 +435,7 @@ int s3od_layernorm_fwd(int dtype, const float* x, const float* w, const float* b
 // ws: S3OD_NREP * 2 * D floats (replicated dw / db partials), all zero on entry; left all zero
 int s3od_layernorm_bwd(int dtype, const void* dy, const float* x, const float* mean, const float* rstd, const float* w,
                        const float* dres, float* dx, float* dw, float* db, float* ws, int M, int D_, void* stream) {
-  static const int rpb = dev_knob("S3OD_LN_RPB", 32);
+  const int rpb = S3OD_KNOB("S3OD_LN_RPB", 32);
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_D(D_, {
     DISPATCH_T(dtype, {
@@ -455,7 +455,7 @@ int s3od_layernorm_ls_bwd(int dtype, const void* dy, const float* x, const float
   S3OD_REQUIRE(u && lam && du && ws2 && ws != ws2, "layernorm_ls_bwd: bad arguments");
   // rows per block: 64 (bf16, M 65616: 221 us vs 240 us at 32 and 328 us at 16; the fused kernel runs at 3
   // waves/SIMD, so longer blocks amortise the 4 x D partial flush)
-  static const int rpb = dev_knob("S3OD_LNLS_RPB", 64);
+  const int rpb = S3OD_KNOB("S3OD_LNLS_RPB", 64);
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_D(D_, {
     DISPATCH_T(dtype, {
@@ -491,7 +491,7 @@ int s3od_colsum(int dtype, const void* a, long lda, int M, int N, float* out, vo
 // ws: S3OD_NREP * 2 * D floats (replicated dlam / dbias partials), all zero on entry; left all zero
 int s3od_layerscale_bwd(int dtype, const float* dx, const void* u, const float* lam, void* du, float* dlam, float* dbias,
                         float* ws, int M, int D_, void* stream) {
-  static const int rpb = dev_knob("S3OD_LS_RPB", 16);
+  const int rpb = S3OD_KNOB("S3OD_LS_RPB", 16);
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_D(D_, {
     DISPATCH_T(dtype, {
@@ -509,7 +509,7 @@ int s3od_qkv_unrope(int dtype, const void* dq, const void* dk, const void* dv, c
   S3OD_REQUIRE(H == 12 || H == 16, "qkv_unrope: %d heads not built (12 or 16)", H);
   const long M = (long)B * Ntok;
   const int D_ = 64 * H;
-  const int rpb = dev_knob("S3OD_UNROPE_RPB", 64);
+  const int rpb = S3OD_KNOB("S3OD_UNROPE_RPB", 64);
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     if (H == 12)

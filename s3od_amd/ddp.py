@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import time
 
 import torch
 import torch.distributed as dist
@@ -52,6 +53,7 @@ class GradSync:
     def on_ready(self, name, flat_slice):
         if not self.enabled or (self.world == 1 and not self.rehearse):
             return
+        nbytes = flat_slice.numel() * flat_slice.element_size()
         if flat_slice.is_cuda:
             if self.stream is None:
                 self.stream = torch.cuda.Stream(device=flat_slice.device)
@@ -65,53 +67,107 @@ class GradSync:
                     e0.record(self.stream)
                 w = dist.all_reduce(flat_slice, op=op, group=self.group, async_op=True)
                 if self.timing:
+                    # ProcessGroupNCCL runs the collective on its own internal stream: wait() makes the comm
+                    # stream wait for the collective's end event, so e0 -> e1 spans the RCCL kernel itself
+                    # (e0 fires once the bucket is ready AND the previous bucket's collective has ended)
+                    w.wait()
                     e1.record(self.stream)
-                    self._ev.append((name, flat_slice.numel() * flat_slice.element_size(), e0, e1))
+                    self._ev.append((len(self._join), name, nbytes, e0, e1))
         else:
+            t0 = time.perf_counter()
             w = dist.all_reduce(flat_slice, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            if self.timing:
+                self._ev.append((len(self._join), name, nbytes, t0, w))
         self.works.append((w, flat_slice))
 
     def finish(self):
-        timed = self.timing and self.stream is not None and bool(self.works)
+        timed = self.timing and bool(self.works)
+        cuda = self.stream is not None
         if timed:
-            eb = torch.cuda.Event(enable_timing=True)
-            eb.record()
+            if cuda:
+                eb = torch.cuda.Event(enable_timing=True)
+                eb.record()
+            else:
+                eb = time.perf_counter()
+        done = {}
         for w, t in self.works:
             w.wait()
+            if not cuda:
+                done[id(w)] = time.perf_counter()      # host clock: issue -> wait() return (gloo, CPU tensors)
             if self.backend != "nccl":
                 t.div_(self.world)
-        if self.stream is not None:
+        if cuda:
             torch.cuda.current_stream().wait_stream(self.stream)
         if timed:
-            ej = torch.cuda.Event(enable_timing=True)
-            ej.record()
+            if cuda:
+                ej = torch.cuda.Event(enable_timing=True)
+                ej.record()
+            else:
+                ej = time.perf_counter()
+                self._ev = [(s, n, b, t0, done.get(id(w), ej) if not isinstance(w, float) else w)
+                            for s, n, b, t0, w in self._ev]
             self._join.append((eb, ej))
         self.works.clear()
 
     def reset_timing(self, on=True):
         self.timing, self._ev, self._join = on, [], []
 
+    @staticmethod
+    def _union_ms(iv):
+        """Length of the union of [start, end) intervals (ms)."""
+        tot, cur_s, cur_e = 0.0, None, None
+        for s, e in sorted(iv):
+            if cur_e is None or s > cur_e:
+                if cur_e is not None:
+                    tot += cur_e - cur_s
+                cur_s, cur_e = s, e
+            else:
+                cur_e = max(cur_e, e)
+        if cur_e is not None:
+            tot += cur_e - cur_s
+        return tot
+
     def timing_report(self):
-        """Per-bucket all-reduce time on the comm stream and the exposed communication per step (the compute
-        stream's wait from backward end to the join), averaged over the recorded steps (synchronises)."""
+        """Communication report of the timed steps (synchronises).
+
+        * ``buckets[].ms``: per bucket, the mean time from the bucket's all-reduce starting on the comm stream (bucket
+          ready and the previous collective done) to the collective's end (CUDA: HIP events, the end one recorded on
+          the comm stream behind ``Work.wait()``; gloo/CPU: host clock, issue -> ``wait()`` return);
+        * ``allreduce_ms_per_step``: the union of the step's bucket intervals (time the link is busy), mean over steps;
+        * ``bus_GBps``: 2 (N - 1) / N x bytes / that union;
+        * ``comm_exposed_ms`` (+ ``_max``): the compute stream's wait from the end of the backward to the join in
+          ``finish()`` -- the communication the backward did not hide."""
         if not self._join:
             return None
-        torch.cuda.synchronize()
+        cuda = self.stream is not None
+        if cuda:
+            torch.cuda.synchronize()
         steps = len(self._join)
-        per = {}
-        for name, nb, e0, e1 in self._ev:
+        per, by_step = {}, {}
+        origin = {}
+        for s, name, nb, a, b in self._ev:
+            if cuda:
+                ref = origin.setdefault(s, a)    # the step's first bucket start (the comm stream runs buckets in order)
+                t0, t1 = ref.elapsed_time(a), ref.elapsed_time(b)
+            else:
+                t0, t1 = a * 1e3, b * 1e3
             d = per.setdefault(name, {"bytes": nb, "ms": 0.0, "calls": 0})
-            d["ms"] += e0.elapsed_time(e1)
+            d["ms"] += t1 - t0
             d["calls"] += 1
-        exposed = [eb.elapsed_time(ej) for eb, ej in self._join]
+            by_step.setdefault(s, []).append((t0, t1))
+        if cuda:
+            exposed = [eb.elapsed_time(ej) for eb, ej in self._join]
+        else:
+            exposed = [(ej - eb) * 1e3 for eb, ej in self._join]
         buckets = [{"bucket": k, "MB": round(v["bytes"] / 1e6, 2), "ms": round(v["ms"] / max(v["calls"], 1), 3)}
                    for k, v in per.items()]
         tot_b = sum(v["bytes"] for v in per.values())
-        tot_ms = sum(v["ms"] for v in per.values()) / steps
+        tot_ms = sum(self._union_ms(iv) for iv in by_step.values()) / steps
         return {"steps": steps, "buckets": buckets, "allreduce_ms_per_step": round(tot_ms, 3),
                 "allreduce_MB_per_step": round(tot_b / 1e6, 2),
                 "bus_GBps": round(tot_b / 1e6 / tot_ms * 2 * (self.world - 1) / self.world, 1) if tot_ms > 0 and self.world > 1 else None,
-                "comm_exposed_ms": round(sum(exposed) / steps, 3), "comm_exposed_ms_max": round(max(exposed), 3)}
+                "comm_exposed_ms": round(sum(exposed) / steps, 3), "comm_exposed_ms_max": round(max(exposed), 3),
+                "clock": "HIP events" if cuda else "host perf_counter"}
 
 
 def broadcast_parameters(model, src=0, group=None):

@@ -12,13 +12,14 @@ Reference structure: src/s3od/model.py:62-467 and tf:models/dinov3_vit/modeling_
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 from dataclasses import dataclass, field
 
 import torch
 
-from ._lib import lib, stream, F32, BF16
+from ._lib import lib, stream, F32, BF16, NREP
 from .weights import OUT_CH, VARIANTS
 
 NREG = 4
@@ -58,6 +59,8 @@ class DPTEngine:
         self._wkey = None
         self._zpool = {}       # persistent all-zero workspaces (the kernels that read them back leave them zero)
         self._nbt = []         # BatchNorm num_batches_tracked counters to bump once per forward
+        self._slabs = {}       # hipStream_t -> split-K slab workspace (contents dead between calls)
+        self._slab_need = {}   # shape key -> slab bytes the library asks for
 
     def zero_ws(self, key, n, dtype, dev):
         """Persistent workspace of >= n elements that is all zero between calls: every C-ABI entry given one
@@ -327,7 +330,7 @@ class DPTEngine:
         return out
 
     def _conv_bn_train(self, x, wt, B, h, w, bias, relu_in=False):
-        stats = self.zero_ws("bn_stats", 32 * 2 * 256, torch.float64, x.device)   # S3OD_NREP replicas, cleared by s3od_bn_finalize
+        stats = self.zero_ws("bn_stats", NREP * 2 * 256, torch.float64, x.device)   # S3OD_NREP replicas, cleared by s3od_bn_finalize
         z = self._conv(x, wt, B, h, w, 256, 256, 3, 1, 1, bias=bias, relu_in=relu_in, stats=stats)
         return dict(z=z, stats=stats)
 
@@ -463,8 +466,27 @@ class DPTEngine:
     def _colsum(self, a, M, N, out, lda=None):
         lib()("s3od_colsum", self.dt, a, lda or N, M, N, out, stream())
 
+    def _slab(self, entry, key, *args):
+        """Caller-owned split-K slab workspace for a weight-gradient entry (the C ABI never allocates): sized by the
+        library's own query (s3od_linear_wgrad_ws / s3od_conv_wgrad_ws; cached per shape), one buffer per stream --
+        calls on one stream run in order, and the main and side streams both issue weight gradients.  Allocated
+        under the stream that uses it, so the caching allocator orders any later reuse behind that stream."""
+        nb = self._slab_need.get(key)
+        if nb is None:
+            n = ctypes.c_long(0)
+            lib()(entry, *args, ctypes.addressof(n))
+            nb = self._slab_need[key] = int(n.value)
+        if nb == 0:
+            return None, 0
+        st = torch.cuda.current_stream()
+        t = self._slabs.get(st.cuda_stream)
+        if t is None or t.numel() * 4 < nb:
+            t = self._slabs[st.cuda_stream] = torch.empty(nb // 4, dtype=torch.float32, device=st.device)
+        return t, t.numel() * 4
+
     def _wgrad_lin(self, dy, x, Nout, Kin, rows, dw, lddy=None, ldx=None):
-        lib()("s3od_linear_wgrad", self.dt, Nout, Kin, rows, dy, lddy or Nout, x, ldx or Kin, dw, 0, stream())
+        slab, nb = self._slab("s3od_linear_wgrad_ws", ("lin", self.dt, Nout, Kin, rows), self.dt, Nout, Kin, rows, 0)
+        lib()("s3od_linear_wgrad", self.dt, Nout, Kin, rows, dy, lddy or Nout, x, ldx or Kin, dw, 0, slab, nb, stream())
 
     def _dgrad_lin(self, dy, w, M, N, K, out, act=ACT_NONE, aux=None, out_f32=False, row_mode=0, P=0, prefix=0, ldaux=None,
                    colsum=None):
@@ -474,7 +496,10 @@ class DPTEngine:
     def _wgrad_conv(self, dy, x, B, H, W, Cin, OH, OW, Cout, k, s, p, dw, relu_x=False):
         # taps > 1: fp32 workspace in the GEMM's [Cout][tap][Cin] layout (contiguous split-K atomics), zero between calls
         ws = self.zero_ws("wgrad", Cout * k * k * Cin, torch.float32, dy.device) if k > 1 else None
-        lib()("s3od_conv_wgrad", self.dt, B, H, W, Cin, OH, OW, Cout, k, k, s, p, dy, x, int(relu_x), dw, ws, 0, stream())
+        slab, nb = self._slab("s3od_conv_wgrad_ws", ("conv", self.dt, B, H, W, Cin, OH, OW, Cout, k, s, p),
+                              self.dt, B, H, W, Cin, OH, OW, Cout, k, k, s, p, 0)
+        lib()("s3od_conv_wgrad", self.dt, B, H, W, Cin, OH, OW, Cout, k, k, s, p, dy, x, int(relu_x), dw, ws, 0, slab, nb,
+              stream())
 
     def _dgrad_conv(self, dy, w, B, H, W, Cin, OH, OW, Cout, k, s, p, act=ACT_NONE, res1=None, out=None, colsum=None,
                     wT=None):
@@ -503,7 +528,7 @@ class DPTEngine:
         h, w = c["h"], c["w"]
         npix = B * h * w
         dev = d_out.device
-        sums = self.zero_ws("bn_sums", 32 * 3 * 256, torch.float64, dev)   # S3OD_NREP replicas, zero between calls
+        sums = self.zero_ws("bn_sums", NREP * 3 * 256, torch.float64, dev)   # S3OD_NREP replicas, zero between calls
         dz2 = torch.empty_like(d_out)
         L("s3od_bn_bwd", self.dt, d_out, c["z2"], None, c["bn2"]["mean"], c["bn2"]["rstd"], P[q + "bn2.weight"], sums, dz2,
           G[q + "bn2.weight"], G[q + "bn2.bias"], G[q + "conv2.bias"], npix, 256, st)
@@ -693,9 +718,9 @@ class DPTEngine:
         dxi = _E(None, (B, Nt, D), torch.float32, dev)
         dqkv = _E(None, (M, 3 * D), T, dev)
         delta = _E(None, (B * H, Nt), torch.float32, dev)
-        qv_ws = self.zero_ws("qv", 32 * 2 * D, torch.float32, dev)     # S3OD_NREP replicas of the q/v bias partials
-        red_ws = self.zero_ws("red", 32 * 2 * D, torch.float32, dev)   # same, for LayerNorm / LayerScale parameter grads
-        red2_ws = self.zero_ws("red2", 32 * 2 * D, torch.float32, dev)  # the LayerScale half of the fused LN + LS backward
+        qv_ws = self.zero_ws("qv", NREP * 2 * D, torch.float32, dev)     # S3OD_NREP replicas of the q/v bias partials
+        red_ws = self.zero_ws("red", NREP * 2 * D, torch.float32, dev)   # same, for LayerNorm / LayerScale parameter grads
+        red2_ws = self.zero_ws("red2", NREP * 2 * D, torch.float32, dev)  # the LayerScale half of the fused LN + LS backward
         ls_done = False       # the layer's layer_scale2 backward already ran inside the layer above's norm1 backward
         for i in reversed(range(self.last)):
             if i + 1 in tap_of:
@@ -788,5 +813,11 @@ class DPTEngine:
                         self.grad_hook("seg_head")
             self.encoder_backward(ctx, dtaps, G)
         except BaseException:
+            # side-stream weight gradients may still read ctx activations / workspaces and add into G: the main
+            # stream waits for them before anything is freed (ctx, zero workspaces) or re-used by a retry
+            side = getattr(self, "_side", None)
+            if side is not None:
+                torch.cuda.current_stream(side.device).wait_stream(side)
+            self._wg = DPTEngine._wg
             self._invalidate()
             raise

@@ -4,6 +4,10 @@ from pathlib import Path
 
 import pytest
 
+# the tests A/B kernels by toggling S3OD_* dispatch knobs between calls in one process: S3OD_AB=1 makes the library
+# re-read its knobs per call (it reads them once otherwise; s3od_amd/csrc/common.hpp S3OD_KNOB)
+os.environ.setdefault("S3OD_AB", "1")
+
 REPO = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(REPO))
 GOLDEN = REPO / "tests" / "golden"

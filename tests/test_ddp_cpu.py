@@ -162,3 +162,57 @@ def test_nan_guard_all_ranks_raise_gloo_world2():
     for p in ps:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def _worker_timing(rank, world, port, q):
+    """GradSync's communication report at world 2 (gloo, CPU): the keys bench.py's `comm` object carries, per-bucket
+    intervals that end after they start, and the per-step link-busy time as the UNION of the bucket intervals (never
+    more than their sum)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from s3od_amd.ddp import GradSync
+        sync = GradSync()
+        sync.reset_timing(True)
+        flat = torch.ones(3 << 20, dtype=torch.float32) * (rank + 1)
+        for _ in range(2):                                   # two "steps"
+            sync.on_ready("seg_head", flat[2 << 20:])
+            sync.on_ready("layer0", flat[1 << 20:2 << 20])
+            sync.on_ready("embeddings", flat[:1 << 20])
+            sync.finish()
+        rep = sync.timing_report()
+        sync.reset_timing(False)
+        q.put((rank, rep, float(flat[0])))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gradsync_timing_report_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker_timing, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, rep, v0 in res:
+        assert v0 == pytest.approx(1.5)                      # mean of 1 and 2, then the mean of 1.5 and 1.5
+        assert rep is not None and rep["steps"] == 2
+        for k in ("buckets", "allreduce_ms_per_step", "allreduce_MB_per_step", "bus_GBps", "comm_exposed_ms",
+                  "comm_exposed_ms_max", "clock"):
+            assert k in rep, k
+        assert [b["bucket"] for b in rep["buckets"]] == ["seg_head", "layer0", "embeddings"]
+        assert all(b["ms"] >= 0 for b in rep["buckets"])
+        assert rep["allreduce_MB_per_step"] == pytest.approx(3 * 4 * (1 << 20) / 1e6, rel=1e-3)
+        assert 0 < rep["allreduce_ms_per_step"] <= sum(b["ms"] for b in rep["buckets"]) + 1e-6
+        assert rep["bus_GBps"] is not None and rep["bus_GBps"] > 0
+        assert rep["comm_exposed_ms"] >= 0
+
+
+def test_union_of_intervals():
+    from s3od_amd.ddp import GradSync
+    assert GradSync._union_ms([(0, 2), (1, 3), (5, 6)]) == 4
+    assert GradSync._union_ms([(5, 6), (0, 1)]) == 2
+    assert GradSync._union_ms([]) == 0

@@ -97,7 +97,7 @@ def test_conv_wgrad_halo(cout, B, H, W, relu):
     dw0 = torch.randn(cout, 64, 3, 3, device="cuda", generator=g)
     dw = dw0.clone()
     ws = torch.zeros(cout * 9 * 64, device="cuda")                 # all zero on entry, left all zero
-    lib()("s3od_conv_wgrad", BF16, B, H, W, 64, H, W, cout, 3, 3, 1, 1, _nhwc(dy), _nhwc(x), int(relu), dw, ws, 0, stream())
+    lib()("s3od_conv_wgrad", BF16, B, H, W, 64, H, W, cout, 3, 3, 1, 1, _nhwc(dy), _nhwc(x), int(relu), dw, ws, 0, None, 0, stream())
     torch.cuda.synchronize()
     assert int((ws != 0).sum()) == 0, "conv_wgrad must leave its workspace all zero"
     got = dw - dw0
@@ -117,7 +117,7 @@ def test_conv_wgrad_halo_channel_blocks(cin, cout, B, H, W, relu):
     ref = torch.nn.grad.conv2d_weight(xin, (cout, cin, 3, 3), dy.float(), padding=1)
     dw = torch.zeros(cout, cin, 3, 3, device="cuda")
     ws = torch.zeros(cout * 9 * cin, device="cuda")                # all zero on entry, left all zero
-    lib()("s3od_conv_wgrad", BF16, B, H, W, cin, H, W, cout, 3, 3, 1, 1, _nhwc(dy), _nhwc(x), int(relu), dw, ws, 0, stream())
+    lib()("s3od_conv_wgrad", BF16, B, H, W, cin, H, W, cout, 3, 3, 1, 1, _nhwc(dy), _nhwc(x), int(relu), dw, ws, 0, None, 0, stream())
     torch.cuda.synchronize()
     assert int((ws != 0).sum()) == 0, "conv_wgrad must leave its workspace all zero"
     assert float((dw - ref).abs().max() / ref.abs().max()) < 2e-3, float((dw - ref).abs().max() / ref.abs().max())
@@ -228,7 +228,7 @@ def test_conv_4s2_wgrad(B, H, W):
             dw0 = torch.randn(128, 64, 4, 4, device="cuda", generator=g)
             dw = dw0.clone()
             ws = torch.zeros(128 * 16 * 64, device="cuda")
-            lib()("s3od_conv_wgrad", BF16, B, 2 * H, 2 * W, 64, H, W, 128, 4, 4, 2, 1, _nhwc(dy), _nhwc(x), 0, dw, ws, 0,
+            lib()("s3od_conv_wgrad", BF16, B, 2 * H, 2 * W, 64, H, W, 128, 4, 4, 2, 1, _nhwc(dy), _nhwc(x), 0, dw, ws, 0, None, 0,
                   stream())
             torch.cuda.synchronize()
         finally:

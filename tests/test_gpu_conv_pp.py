@@ -111,17 +111,23 @@ def test_conv_wgrad_pp(B, H, W, Ci, relu):
     dw0 = torch.randn(Co, Ci, 3, 3, device="cuda", generator=g)
     ref = dw0 + torch.nn.grad.conv2d_weight(xin, (Co, Ci, 3, 3), dy.float(), padding=1)
     ws = torch.zeros(Co * 9 * Ci, device="cuda")
+    import ctypes
+    nb = ctypes.c_long(0)
+    lib()("s3od_conv_wgrad_ws", BF16, B, H, W, Ci, H, W, Co, 3, 3, 1, 1, 0, ctypes.addressof(nb))
+    # the caller-owned split-K slab (poisoned: every word read back must have been written)
+    slab = torch.full((max(nb.value, 4) // 4,), float("nan"), device="cuda") if nb.value else None
     outs = {}
-    for knob in ("1", "0"):
+    for knob, sl in (("1", None), ("1", slab), ("0", None)):
         dw = dw0.clone()
         os.environ["S3OD_WGRAD_PP"] = knob
         try:
-            lib()("s3od_conv_wgrad", BF16, B, H, W, Ci, H, W, Co, 3, 3, 1, 1, _nhwc(dy), _nhwc(x), relu, dw, ws, 0, stream())
+            lib()("s3od_conv_wgrad", BF16, B, H, W, Ci, H, W, Co, 3, 3, 1, 1, _nhwc(dy), _nhwc(x), relu, dw, ws, 0, sl,
+                  nb.value if sl is not None else 0, stream())
         finally:
             os.environ.pop("S3OD_WGRAD_PP", None)
         torch.cuda.synchronize()
         err = float((dw - ref).norm() / (ref - dw0).norm())
-        assert err < 1e-5, (knob, err)
-        outs[knob] = dw
+        assert err < 1e-5, (knob, sl is not None, err)
+        outs[knob, sl is not None] = dw
     assert float(ws.abs().max()) == 0.0          # the workspace is left all zero
-    assert float((outs["1"] - outs["0"]).norm() / (ref - dw0).norm()) < 1e-5
+    assert float((outs["1", False] - outs["0", False]).norm() / (ref - dw0).norm()) < 1e-5

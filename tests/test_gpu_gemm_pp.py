@@ -124,15 +124,29 @@ def test_pp_linear_dgrad_gelu_bwd():
     assert rel_l2(dx.float(), g) < 5e-3
 
 
+def _wgrad_slab(L, Nout, Kin, rows):
+    """Caller-owned split-K slab sized by the library's own query (s3od_linear_wgrad_ws), poisoned with NaN: the
+    kernel must overwrite every word it reads back."""
+    import ctypes
+    n = ctypes.c_long(0)
+    L("s3od_linear_wgrad_ws", BF16, Nout, Kin, rows, 0, ctypes.addressof(n))
+    return n.value, (torch.full((max(n.value, 4) // 4,), float("nan"), device="cuda") if n.value else None)
+
+
+@pytest.mark.parametrize("slab", [False, True])
 @pytest.mark.parametrize("Nout,Kin,rows", [(3072, 768, 16384 + 80), (768, 3072, 16384 + 80), (2304, 768, 20000)])
-def test_pp_linear_wgrad_split(Nout, Kin, rows):
-    """split-K wgrad (fp32 atomics) accumulating onto an existing gradient."""
+def test_pp_linear_wgrad_split(Nout, Kin, rows, slab):
+    """split-K wgrad accumulating onto an existing gradient: fp32 atomics (no slab passed) and the per-split slabs in a
+    caller-owned workspace + the reduce kernel (slab = True; the C ABI never allocates)."""
     torch.manual_seed(rows)
     L, s = _lib()
     dy, x = r(rows, Nout), r(rows, Kin)
     dw0 = r(Nout, Kin, dt=torch.float32)
     dw = dw0.clone()
-    L("s3od_linear_wgrad", BF16, Nout, Kin, rows, dy, Nout, x, Kin, dw, 0, s)
+    nb, ws = _wgrad_slab(L, Nout, Kin, rows) if slab else (0, None)
+    if slab:
+        assert nb > 0 and nb % (4 * Nout * Kin) == 0      # sp slabs of Nout x Kin fp32
+    L("s3od_linear_wgrad", BF16, Nout, Kin, rows, dy, Nout, x, Kin, dw, 0, ws, nb, s)
     ref = dw0 + dy.float().t() @ x.float()
     torch.cuda.synchronize()
     assert rel_l2(dw, ref) < 1e-5
@@ -220,7 +234,8 @@ def test_pp_production_rows_65616():
     # up-projection wgrad over all 65616 rows
     dw0 = r(F, D, dt=torch.float32)
     dw = dw0.clone()
-    L("s3od_linear_wgrad", BF16, F, D, M, dh, F, x, D, dw, 0, s)
+    nb, slab = _wgrad_slab(L, F, D, M)
+    L("s3od_linear_wgrad", BF16, F, D, M, dh, F, x, D, dw, 0, slab, nb, s)
     torch.cuda.synchronize()
     assert rel_l2(dw, dw0 + dh.float().t() @ x.float()) < 1e-5
 

@@ -5,6 +5,7 @@ settings of one per-call environment knob, alternating rounds (dev tool).
     AB_MODE=infer AB_BATCH=8 AB_SIZE=1024 python tools/ab_step.py S3OD_POOL_PRE 0 1   # eval forward (C2 / C5)
 """
 import os
+os.environ.setdefault("S3OD_AB", "1")   # knobs toggled per call (csrc/common.hpp S3OD_KNOB)
 import sys
 import time
 from pathlib import Path

@@ -5,6 +5,7 @@ implicit GEMM (S3OD_CONV_RW=0, read per call), in one process, interleaved round
     python tools/conv64_bench.py [B] [H]
 """
 import os
+os.environ.setdefault("S3OD_AB", "1")   # knobs toggled per call (csrc/common.hpp S3OD_KNOB)
 import sys
 from pathlib import Path
 

@@ -5,6 +5,7 @@ call), one process, interleaved rounds; outputs compared (dev tool).
     python tools/convT_bench.py [B] [H]
 """
 import os
+os.environ.setdefault("S3OD_AB", "1")   # knobs toggled per call (csrc/common.hpp S3OD_KNOB)
 import sys
 from pathlib import Path
 

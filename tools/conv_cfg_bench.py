@@ -7,6 +7,7 @@ S3OD_CONV_PP values to alternate (read per call).
     python tools/conv_cfg_bench.py 0 1 0 1
 """
 import os
+os.environ.setdefault("S3OD_AB", "1")   # knobs toggled per call (csrc/common.hpp S3OD_KNOB)
 import sys
 from pathlib import Path
 
@@ -64,7 +65,7 @@ def wgrad(tag, B, hh, Cin, Cout, relu=0):
     x = torch.randn(B, hh, hh, Cin, device="cuda", generator=g).bfloat16()
     dw = torch.zeros(Cout, Cin, 3, 3, device="cuda")
     ws = torch.zeros(Cout * 9 * Cin, device="cuda")
-    f = lambda: lib()("s3od_conv_wgrad", BF16, B, hh, hh, Cin, hh, hh, Cout, 3, 3, 1, 1, dy, x, relu, dw, ws, 0, stream())
+    f = lambda: lib()("s3od_conv_wgrad", BF16, B, hh, hh, Cin, hh, hh, Cout, 3, 3, 1, 1, dy, x, relu, dw, ws, 0, None, 0, stream())
     t = timeit(f)
     fl = 2.0 * B * hh * hh * Cin * Cout * 9
     print(f"cfg={os.environ.get('S3OD_WGRAD_PP', 'def')} {tag:28s} {t * 1e6:8.1f} us {fl / t / 1e12:7.1f} TF/s", flush=True)

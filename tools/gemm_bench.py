@@ -48,7 +48,7 @@ def wgrad(Nout, Kin, rows):
     dy = torch.randn(rows, Nout, device="cuda").bfloat16()
     x = torch.randn(rows, Kin, device="cuda").bfloat16()
     dw = torch.zeros(Nout, Kin, device="cuda")
-    f = lambda: lib()("s3od_linear_wgrad", BF16, Nout, Kin, rows, dy, Nout, x, Kin, dw, 0, stream())
+    f = lambda: lib()("s3od_linear_wgrad", BF16, Nout, Kin, rows, dy, Nout, x, Kin, dw, 0, None, 0, stream())
     t = timeit(f)
     print(f"linear wgrad N={Nout} K={Kin} rows={rows}: {t * 1e6:8.1f} us  {2 * Nout * Kin * rows / t / 1e12:7.1f} TF/s")
 
@@ -106,7 +106,7 @@ def check():
         rd = dy.float() @ w.float()
         e2 = ((dx - rd).norm() / rd.norm()).item()
         dw = torch.zeros(N, K, device="cuda")
-        lib()("s3od_linear_wgrad", BF16, N, K, M, dy, N, x, K, dw, 0, stream())
+        lib()("s3od_linear_wgrad", BF16, N, K, M, dy, N, x, K, dw, 0, None, 0, stream())
         rw = dy.float().t() @ x.float()
         e3 = ((dw - rw).norm() / rw.norm()).item()
         torch.cuda.synchronize()

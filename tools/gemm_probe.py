@@ -37,7 +37,7 @@ def main():
     elif op == "wgrad":
         dy, x = r(K, M), r(K, N)
         dw = torch.zeros(M, N, device="cuda")
-        f = lambda: L("s3od_linear_wgrad", BF16, M, N, K, dy, M, x, N, dw, 0, st)
+        f = lambda: L("s3od_linear_wgrad", BF16, M, N, K, dy, M, x, N, dw, 0, None, 0, st)
     elif op in ("conv", "convw"):
         B = 16
         hh = int(math.isqrt(M // B))
@@ -51,7 +51,7 @@ def main():
             dy = r(B, hh, hh, N)
             dw = torch.zeros(N, K, 3, 3, device="cuda")
             ws = torch.zeros(N * 9 * K, device="cuda")
-            f = lambda: L("s3od_conv_wgrad", BF16, B, hh, hh, K, hh, hh, N, 3, 3, 1, 1, dy, x, 0, dw, ws, 0, st)
+            f = lambda: L("s3od_conv_wgrad", BF16, B, hh, hh, K, hh, hh, N, 3, 3, 1, 1, dy, x, 0, dw, ws, 0, None, 0, st)
     else:
         raise SystemExit(f"unknown op {op}")
     for _ in range(reps):

@@ -55,6 +55,26 @@ REF = {
     "s3od_eval_metrics": "EvaluationMetrics.step (MAE, MaxF/AvgF, S-measure) + EMeasure + WeightedFMeasure on device: synth_sod/src/synth_sod/model_training/metrics.py:14-424",
     "s3od_eval_metrics_ws": "scratch size of s3od_eval_metrics (new; the reference allocates numpy temporaries)",
     "s3od_preprocess": "BackgroundRemoval._preprocess normalisation: src/s3od/predictor.py:79-94",
+    "s3od_linear_wgrad_ws": "workspace query of s3od_linear_wgrad: bytes of the caller-owned split-K slab (new; PyTorch autograd allocates internally)",
+    "s3od_conv_wgrad_ws": "workspace query of s3od_conv_wgrad: bytes of the caller-owned split-K slab (new; PyTorch autograd allocates internally)",
+    "s3od_token_prefix_bwd": "cat([cls, register_tokens, patches]) backward: tf:modeling_dinov3_vit.py:88-92 (reference: implicit torch autograd)",
+    "s3od_layernorm_ls_bwd": "norm2 / norm1 LayerNorm backward fused with the DINOv3ViTLayerScale backward that consumes its dx: tf:modeling_dinov3_vit.py:337-343, 419-445 (reference: implicit torch autograd)",
+}
+
+# caller-owned buffers whose size is not implied by the other arguments (a non-Python caller sizes them
+# from this header).  NREP = S3OD_NREP replicas (#define below).
+WS = {
+    "s3od_conv_fwd": "stats (nullable): fp64 [S3OD_NREP][2][Cout] (sum | sum of squares replicas), all zero on entry; s3od_bn_finalize folds and clears it",
+    "s3od_bn_finalize": "stats: the fp64 [S3OD_NREP][2][C] replicas s3od_conv_fwd filled; read and left all zero",
+    "s3od_bn_bwd": "sums: fp64 [S3OD_NREP][3][C], all zero on entry, left all zero",
+    "s3od_bn_relu_bwd": "sums: fp64 [S3OD_NREP][3][C], all zero on entry, left all zero",
+    "s3od_layernorm_bwd": "ws: fp32 [S3OD_NREP][2][D], all zero on entry, left all zero",
+    "s3od_layernorm_ls_bwd": "ws, ws2: fp32 [S3OD_NREP][2][D] each (LayerNorm dw|db and LayerScale dlam|dbias replicas), all zero on entry, left all zero",
+    "s3od_layerscale_bwd": "ws: fp32 [S3OD_NREP][2][D], all zero on entry, left all zero",
+    "s3od_qkv_unrope": "ws: fp32 [S3OD_NREP][2][64 H], all zero on entry, left all zero",
+    "s3od_attn_bwd_qkv": "ws: fp32 [S3OD_NREP][2][64 H], all zero on entry, left all zero",
+    "s3od_conv_wgrad": "ws (nullable): fp32 [Cout][KH][KW][Cin], all zero on entry, left all zero; slab (nullable): >= s3od_conv_wgrad_ws bytes, contents dead between calls",
+    "s3od_linear_wgrad": "slab (nullable): >= s3od_linear_wgrad_ws bytes, contents dead between calls (without it the split-K partials are fp32 atomics into dw)",
 }
 
 SIG = re.compile(r"^(int|const char\*)\s+(s3od_\w+)\(([^)]*)\)\s*\{", re.M | re.S)
@@ -73,6 +93,11 @@ def collect():
     return out
 
 
+def nrep():
+    m = re.search(r"constexpr int S3OD_NREP = (\d+);", (ROOT / "s3od_amd" / "csrc" / "common.hpp").read_text())
+    return int(m.group(1))
+
+
 def main():
     decls = collect()
     lines = [
@@ -80,7 +105,8 @@ def main():
         " * GENERATED by tools/gen_header.py from s3od_amd/csrc/*.hip; do not edit by hand.",
         " *",
         " * Conventions: device pointers only; the caller (PyTorch caching allocator) owns every",
-        " * buffer; kernels never allocate.  `stream` is a hipStream_t.  dtype: 0 = f32 (strict",
+        " * buffer, workspaces included (sizes stated per entry below or returned by a *_ws query):",
+        " * the library never allocates.  `stream` is a hipStream_t.  dtype: 0 = f32 (strict",
         " * parity path, v_mfma_f32_16x16x4_f32), 1 = bf16 (fast path, v_mfma_f32_16x16x32_bf16).",
         " * Activations are NHWC; weights are repacked [Cout][KH][KW][Cin] for the kernels while",
         " * gradients are written in the reference (PyTorch state_dict) layout.",
@@ -91,13 +117,16 @@ def main():
         " */",
         "#ifndef S3OD_HIP_H",
         "#define S3OD_HIP_H",
+        "",
+        "/* replicas of the column-sum / BN-statistic accumulation workspaces (sizes below) */",
+        f"#define S3OD_NREP {nrep()}",
         "#ifdef __cplusplus",
         'extern "C" {',
         "#endif",
         "",
     ]
     for name, ret, args, src in decls:
-        lines.append(f"/* {REF.get(name, 'internal')}  [{src}] */")
+        lines.append(f"/* {REF[name]}  [{src}]" + (f"\n * buffers: {WS[name]}" if name in WS else "") + " */")
         lines.append(f"{ret} {name}({args});")
         lines.append("")
     lines += ["#ifdef __cplusplus", "}", "#endif", "#endif  /* S3OD_HIP_H */", ""]

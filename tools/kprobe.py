@@ -29,7 +29,7 @@ if which in ("wgrad64", "conv64"):
     out = torch.empty_like(x)
     for _ in range(3):
         if which == "wgrad64":
-            lib()("s3od_conv_wgrad", BF16, B, H, H, C, H, H, C, 3, 3, 1, 1, dy, x, 0, dw, ws, 0, stream())
+            lib()("s3od_conv_wgrad", BF16, B, H, H, C, H, H, C, 3, 3, 1, 1, dy, x, 0, dw, ws, 0, None, 0, stream())
         else:
             lib()("s3od_conv_fwd", BF16, B, H, H, C, H, H, C, 3, 3, 1, 1, x, 0, w, None, None, None, 1, None, None, out,
                   None, None, None, stream())

@@ -4,6 +4,7 @@ C ABI, for the tile config selected by S3OD_GEMM_CFG (dev tool; run once per con
     S3OD_GEMM_CFG=4 python tools/lin_sweep.py
 """
 import os
+os.environ.setdefault("S3OD_AB", "1")   # knobs toggled per call (csrc/common.hpp S3OD_KNOB)
 import sys
 from pathlib import Path
 
@@ -55,7 +56,7 @@ def dgrad(name, N, K, act=0, out_f32=False, aux=False):
 def wgrad(name, Nout, Kin):
     dy, x = r(M, Nout), r(M, Kin)
     dw = torch.zeros(Nout, Kin, device="cuda")
-    f = lambda: lib()("s3od_linear_wgrad", BF16, Nout, Kin, M, dy, Nout, x, Kin, dw, 0, stream())
+    f = lambda: lib()("s3od_linear_wgrad", BF16, Nout, Kin, M, dy, Nout, x, Kin, dw, 0, None, 0, stream())
     report(name, 2.0 * M * Nout * Kin, timeit(f))
 
 
@@ -88,7 +89,7 @@ def wgrad_conv(name, B, H, Cin, Cout):
     dy, x = r(B, H, H, Cout), r(B, H, H, Cin)
     dw = torch.zeros(Cout * 9 * Cin, device="cuda")
     ws = torch.zeros(Cout * 9 * Cin, device="cuda")
-    f = lambda: lib()("s3od_conv_wgrad", BF16, B, H, H, Cin, H, H, Cout, 3, 3, 1, 1, dy, x, 0, dw, ws, 0, stream())
+    f = lambda: lib()("s3od_conv_wgrad", BF16, B, H, H, Cin, H, H, Cout, 3, 3, 1, 1, dy, x, 0, dw, ws, 0, None, 0, stream())
     report(name, 2.0 * B * H * H * Cout * Cin * 9, timeit(f))
 
 

@@ -5,6 +5,7 @@ Shapes: upsample_2x.2 (1024^2, 64 -> 64) and output_conv1 (512^2, 256 -> 128, Re
     python tools/wgrad_bench.py
 """
 import os
+os.environ.setdefault("S3OD_AB", "1")   # knobs toggled per call (csrc/common.hpp S3OD_KNOB)
 import sys
 from pathlib import Path
 
@@ -39,7 +40,7 @@ def main():
             for knob in ("0", "1"):
                 os.environ["S3OD_WGRAD_DMA"] = knob
                 dw = torch.zeros(cout, cin, 3, 3, device="cuda")
-                f = lambda: lib()("s3od_conv_wgrad", BF16, B, H, H, cin, H, H, cout, 3, 3, 1, 1, dy, x, relu, dw, ws, 0, stream())
+                f = lambda: lib()("s3od_conv_wgrad", BF16, B, H, H, cin, H, H, cout, 3, 3, 1, 1, dy, x, relu, dw, ws, 0, None, 0, stream())
                 t = timeit(f)
                 dw.zero_()
                 f()
@@ -62,7 +63,7 @@ def main():
         for knob in ("0", "1"):
             os.environ["S3OD_WGRAD_DMA"] = knob
             dw = torch.zeros(128, 64, 4, 4, device="cuda")
-            f = lambda: lib()("s3od_conv_wgrad", BF16, B, 2 * H, 2 * H, 64, H, H, 128, 4, 4, 2, 1, dy, x, 0, dw, ws, 0, stream())
+            f = lambda: lib()("s3od_conv_wgrad", BF16, B, 2 * H, 2 * H, 64, H, H, 128, 4, 4, 2, 1, dy, x, 0, dw, ws, 0, None, 0, stream())
             t = timeit(f)
             dw.zero_()
             f()
