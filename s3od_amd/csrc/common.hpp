@@ -124,6 +124,21 @@ static inline bool s3od_ab_mode() {
 // true when the knob is set to 0 (the "off" switch of a specialised path)
 #define S3OD_OFF(name) (S3OD_KNOB(name, 1) == 0)
 
+// ------------------------------------------------------------------ wave synchronisation (hand-pipelined kernels)
+// counted wait on this wave's vector-memory queue (LDS-DMA pieces, loads and stores count together, in issue order)
+template <int N> DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+DEV void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// s_barrier WITHOUT the vmcnt(0) a __syncthreads() emits: LDS-DMA stays in flight across it
+DEV void raw_barrier() { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); }
+DEV void lds_barrier() { wait_lgkm0(); __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); }
+// a segment boundary of a ping-pong schedule: no instruction moves across it (register-only MFMAs included)
+DEV void seg_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // Column reductions over many workgroups add into S3OD_NREP replicas of the accumulator
 // (workgroup b -> replica b % S3OD_NREP) and a second pass folds the replicas: fp32/fp64 atomics
 // from ~1000 workgroups onto the same few KB serialise at the memory side (measured 2-3x slower

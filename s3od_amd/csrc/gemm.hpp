@@ -684,10 +684,7 @@ template <typename T, int BM, int BN, int NST_ = 3, int WM_ = 0> struct GemmShap
 
 struct KRange { int kt0, kt1; };
 
-template <int N> DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-DEV void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 // workgroup barrier that orders LDS only (does not drain in-flight global loads / LDS-DMA)
-DEV void lds_barrier() { wait_lgkm0(); __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); }
 
 // Block-level epilogue contract:  epi(tile, LDT, m0, n0, tid, BM, BN)
 //
@@ -1112,7 +1109,6 @@ template <> struct PPFrag<false> {
   }
 };
 
-DEV void raw_barrier() { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); }
 
 // The epilogue stages C through the K-stage LDS in two 128-row chunks with LDS barriers only (a
 // __syncthreads() would drain the stores).  (A persistent variant -- the next tile's first K

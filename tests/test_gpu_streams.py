@@ -1,8 +1,11 @@
 """GPU: the two-stream backward (weight gradients on a side stream beside the data-gradient chain, DDP buckets hooked
 from the side stream) must give the gradients of the single-stream backward (S3OD_BWD_SIDE=0), parameter by
 parameter: a missing claim() / record_stream would show up as a small, nondeterministic corruption that the
-train-step-vs-oracle tolerances can hide.  The kernels are the same on both paths; only the order of the fp32 split-K
-atomics differs, so the bound is summation-order noise (rel 1e-5)."""
+train-step-vs-oracle tolerances can hide.  The kernels are the same on both paths; only the order of fp32 / fp64
+atomics (split-K weight gradients, BN statistics, bias column sums) differs.  In f32 (strict path) that is summation-order
+noise: rel 1e-5 per parameter.  In bf16 the same noise flips bf16 roundings that the chain amplifies (a single-stream run
+against itself already differs by ~1e-3 rel at layer 0), so the bf16 check compares the side-vs-single difference with
+that run-to-run floor."""
 import os
 
 import pytest
@@ -11,13 +14,13 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _grads(side, bs=2, S=256):
+def _grads(side, bs=2, S=256, dt="bf16"):
     from s3od_amd.model import DPTSegmentation
     from s3od_amd.loss import LossModule, FOCAL_IOU
     os.environ["S3OD_BWD_SIDE"] = "1" if side else "0"
     try:
         torch.manual_seed(0)
-        m = DPTSegmentation(compute_dtype="bf16").cuda().train()
+        m = DPTSegmentation(compute_dtype=dt).cuda().train()
         m._rope_rescale = 1.0
         crit = LossModule(FOCAL_IOU, full_mask_lambda=0.1, decay_rate=0.2)
         g = torch.Generator(device="cuda").manual_seed(5)
@@ -34,14 +37,19 @@ def _grads(side, bs=2, S=256):
         os.environ.pop("S3OD_BWD_SIDE", None)
 
 
-def test_side_stream_backward_equals_single_stream():
-    a, b = _grads(True), _grads(False)
+def _skip(n):
+    # feeds a train-mode BN: the true gradient is 0, every run holds rounding noise
+    return "resConfUnit" in n and (n.endswith("conv1.bias") or n.endswith("conv2.bias"))
+
+
+def test_side_stream_backward_equals_single_stream_f32():
+    a, b = _grads(True, dt="f32"), _grads(False, dt="f32")
     for rep in (0, 1):
         assert a[rep].keys() == b[rep].keys()
         worst = (0.0, None)
         for n in a[rep]:
-            if "resConfUnit" in n and (n.endswith("conv1.bias") or n.endswith("conv2.bias")):
-                continue      # feeds a train-mode BN: the true gradient is 0, both runs hold rounding noise
+            if _skip(n):
+                continue
             x, y = a[rep][n], b[rep][n]
             assert torch.isfinite(x).all(), n
             den = float(y.norm())
@@ -50,3 +58,18 @@ def test_side_stream_backward_equals_single_stream():
                 continue
             worst = max(worst, (float((x - y).norm()) / den, n))
         assert worst[0] < 1e-5, (rep, worst)
+
+
+def test_side_stream_backward_bf16_within_run_to_run_noise():
+    a, b, c = _grads(True), _grads(False), _grads(False)
+    for rep in (0, 1):
+        d_side = d_self = tot = 0.0
+        for n in a[rep]:
+            if _skip(n):
+                continue
+            assert torch.isfinite(a[rep][n]).all(), n
+            d_side += float((a[rep][n] - b[rep][n]).double().pow(2).sum())
+            d_self += float((c[rep][n] - b[rep][n]).double().pow(2).sum())
+            tot += float(b[rep][n].double().pow(2).sum())
+        d_side, d_self, tot = d_side ** 0.5, d_self ** 0.5, tot ** 0.5
+        assert d_side <= 3.0 * d_self + 1e-6 * tot, (rep, d_side / tot, d_self / tot)
