@@ -1203,336 +1203,6 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __res
   }
 }
 
-// ===================================================================================== backward, bf16, 8-wave ping-pong
-// The 4-wave kernels above leave the pairing of matrix and vector work on a SIMD to chance: their two resident
-// workgroups run unsynchronised, so a SIMD often holds two waves in their softmax VALU (matrix pipe idle) or two in
-// their MFMA bursts (65 % MFMA-busy measured, profiles/r03q_attn_bwd_pmc.txt).  These kernels pair them explicitly
-// (MI355X_MICROARCH.md "Two waves per SIMD"): one workgroup of 8 waves per CU, waves w and w + 4 share a SIMD and the
-// same 32 keys (dK/dV) or 32 queries (dQ); wave w takes the first 32-row half of every 64-row tile, wave w + 4 the
-// second.  Each wave alternates an M segment (the previous tile's dV/dK (or dQ) MFMAs + this tile's S / dP MFMAs) and
-// a V segment (exp2, P * dP, bf16 packing), one s_barrier per segment, and the w + 4 half runs one segment behind,
-// so every M segment of one wave has its SIMD partner's V segment beside it.  The tiles stream in by LDS-DMA into a
-// 4-deep ring: the lagging half issues tile j + 3 in its V segment of tile j and retires tile j + 1 (counted vmcnt,
-// tile j + 2 left in flight) at the end of its M segment of tile j, three segments of cover.  The two halves' partial
-// dK / dV (dQ) meet once, through LDS, at the end.
-//
-// Ring reads (segment s, tile j): the leading half reads tile j in s = 2j (S / dP) and 2j + 2 (dV / dK), the lagging
-// half in 2j + 1 and 2j + 3; tile j + 3 (the slot of j - 1, last read in 2j + 1) is issued in 2j + 2 and retired at
-// the end of 2j + 5, before its first read in 2j + 6.
-namespace {
-constexpr int PP_NS = 4;                                   // LDS ring depth (tiles)
-DEV int pp_wave() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
-// logical (row block, bh) of this workgroup: the blocks of one (b, h) on one XCD (blocks b and b + 8 share one under the
-// observed round-robin dispatch; speed only), bijective for any grid size
-DEV void pp_block(int& xb, int& bh) {
-  const int nwg = gridDim.x * gridDim.y, L = blockIdx.y * gridDim.x + blockIdx.x;
-  const int q = nwg >> 3, r = nwg & 7, xcd = L & 7, idx = L >> 3;
-  const int W = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-  bh = W / gridDim.x; xb = W - bh * gridDim.x;
-}
-// exchange one wave's f32x16 pair with its SIMD partner through LDS (1 KiB wave-linear rows: conflict-free)
-DEV void pp_put(char* slot, const f32x16 (&v)[2], int lane) {
-#pragma unroll
-  for (int db = 0; db < 2; db++)
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-      *(f32x4*)(slot + ((db * 4 + c) * 64 + lane) * 16) = f32x4{v[db][4 * c], v[db][4 * c + 1], v[db][4 * c + 2], v[db][4 * c + 3]};
-}
-DEV void pp_add(const char* slot, f32x16 (&v)[2], int lane) {
-#pragma unroll
-  for (int db = 0; db < 2; db++)
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const f32x4 x = *(const f32x4*)(slot + ((db * 4 + c) * 64 + lane) * 16);
-#pragma unroll
-      for (int e = 0; e < 4; e++) v[db][4 * c + e] += x[e];
-    }
-}
-}  // namespace
-
-// dK, dV.  Workgroup = 128 keys of one (b,h) = 4 key groups of 32; wave w and w + 4 hold the key group's K / V
-// fragments (negated, as in attn_bwd_dkdv32_kernel) and split each 64-query tile into halves.
-__global__ void __launch_bounds__(512) attn_bwd_dkdv_pp_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
-                                                             const bf16* __restrict__ V, const bf16* __restrict__ dO,
-                                                             const float* __restrict__ LSE, const float* __restrict__ Dl,
-                                                             bf16* __restrict__ dK, bf16* __restrict__ dV, int N, int H,
-                                                             QkvSink sink) {
-  constexpr int SB = 2 * Img32::BYTES + 2048;               // Q image, dO image, LSE (1 KiB piece), delta (1 KiB piece)
-  static_assert(PP_NS * SB >= 4 * 16384, "dkdv pp: exchange fits the ring");
-  __shared__ __attribute__((aligned(1024))) char smem[PP_NS * SB];
-  int xb, bh;
-  pp_block(xb, bh);
-  const int b = bh / H, hh = bh - b * H;
-  const int lane = threadIdx.x & 63, wave = pp_wave(), wr = wave >> 2, kg = wave & 3, h = lane >> 5;
-  const long ldo = (long)H * 64;
-  const char* qbase = (const char*)(Q + (long)bh * N * 64);
-  const char* obase = (const char*)(dO + (long)b * N * ldo + hh * 64);
-  const unsigned long qtot = (unsigned long)N * 128, otot = ((unsigned long)(N - 1) * ldo + 64) * 2;
-  Dma64R<4> dq_, ddo;
-  dq_.init(128, kg, lane);
-  ddo.init(ldo * 2, kg, lane);
-  const unsigned vrow = lane < 16 ? 16u * lane : 0x80000000u;
-  const int k0 = xb * 128 + kg * 32;
-  bf16x8 kf[4], vf[4];
-  {
-    const int key = k0 + (lane & 31);
-    const bf16* kr = K + ((long)bh * N + key) * 64 + 8 * h;
-    const bf16* vr = V + ((long)bh * N + key) * 64 + 8 * h;
-    bf16x8 z; for (int e = 0; e < 8; e++) z[e] = (bf16)0.f;
-#pragma unroll
-    for (int ks = 0; ks < 4; ks++) {
-      kf[ks] = key < N ? neg8(*(const bf16x8*)(kr + 16 * ks)) : z;
-      vf[ks] = key < N ? neg8(*(const bf16x8*)(vr + 16 * ks)) : z;
-    }
-  }
-  f32x16 dk[2], dv[2];
-#pragma unroll
-  for (int db = 0; db < 2; db++) for (int i = 0; i < 16; i++) { dk[db][i] = 0.f; dv[db][i] = 0.f; }
-  const int T = (N + 63) / 64;
-  // the lagging half's DMA of tile t: Q / dO 2 + 2 pieces per wave, LSE (wave 4) and delta (wave 5) one more
-  auto issue = [&](int t) {
-    char* base = smem + (t % PP_NS) * SB;
-    dq_.issue(qbase, qtot, (long)t * 64, 128, base, kg);
-    ddo.issue(obase, otot, (long)t * 64, ldo * 2, base + Img32::BYTES, kg);
-    if (kg == 0) dma_row64r(LSE + (long)bh * N, N, t * 64, vrow, base + 2 * Img32::BYTES);
-    if (kg == 1) dma_row64r(Dl + (long)bh * N, N, t * 64, vrow, base + 2 * Img32::BYTES + 1024);
-  };
-  // retire all of this wave's DMA but the newest tile's (`keep`: a tile newer than the one needed was issued)
-  auto retire = [&](bool keep) {
-    if (keep) { if (kg < 2) wait_vmcnt<5>(); else wait_vmcnt<4>(); }
-    else wait_vmcnt<0>();
-  };
-  const int qh = 32 * wr;                                    // this wave's query rows in every tile
-  f32x16 s, dp;
-  bf16x8 pa[2], da[2];       // P / -dS of the pending tile (bf16 A operands of dV / dK)
-  bf16x8 bo[2][2], bq[2][2]; // dO / Q of the pending tile, transposed (B operands of dV / dK), read in its V segment
-  bf16x8 ra[4], rc[4];       // Q / dO rows of the current tile (A operands of S / dP)
-  // M segment, part 1: this tile's LDS reads (row fragments + the LSE / delta C blocks straight into s / dp)
-  auto sdp_read = [&](const char* qs_) {
-    const char* dos = qs_ + Img32::BYTES;
-#pragma unroll
-    for (int ks = 0; ks < 4; ks++) { ra[ks] = row32(qs_, qh, ks, lane); rc[ks] = row32(dos, qh, ks, lane); }
-    s = ld16((const float*)(qs_ + 2 * Img32::BYTES) + qh + 4 * h);
-    dp = ld16((const float*)(qs_ + 2 * Img32::BYTES + 1024) + qh + 4 * h);
-  };
-  auto sdp_mma = [&]() {
-#pragma unroll
-    for (int ks = 0; ks < 4; ks++) { s = mma32(ra[ks], kf[ks], s); dp = mma32(rc[ks], vf[ks], dp); }
-  };
-  auto dvdk_mma = [&]() {
-#pragma unroll
-    for (int st = 0; st < 2; st++)
-#pragma unroll
-      for (int db = 0; db < 2; db++) { dv[db] = mma32(pa[st], bo[st][db], dv[db]); dk[db] = mma32(da[st], bq[st][db], dk[db]); }
-  };
-  // V segment: s = LSE - S, dp = delta - dP:  P = exp2(-s); -dS = P * dp; packed; then the transposed reads of the
-  // tile for the next M segment's dV / dK (its data is resident: it was read by rows in the M segment just done)
-  auto softmax = [&](const char* qs_) {
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const float p = fexp2(-s[i]);
-      s[i] = p;
-      dp[i] *= p;
-    }
-#pragma unroll
-    for (int st = 0; st < 2; st++) { pa[st] = pack_acc(s, st); da[st] = pack_acc(dp, st); }
-    const char* dos = qs_ + Img32::BYTES;
-#pragma unroll
-    for (int st = 0; st < 2; st++)
-#pragma unroll
-      for (int db = 0; db < 2; db++) { bo[st][db] = tr32(dos, qh + 16 * st, 32 * db, lane); bq[st][db] = tr32(qs_, qh + 16 * st, 32 * db, lane); }
-    // the packs stay in this segment (LLVM would otherwise sink them past the barrier to their use)
-    asm volatile("" ::"v"(pa[0]), "v"(pa[1]), "v"(da[0]), "v"(da[1]));
-  };
-  // prologue: tiles 0 and 1 in flight, tile 0 retired; the lagging half idles one segment (and issues tile 2)
-  if (wr) { issue(0); if (T > 1) issue(1); retire(T > 1); }
-  seg_barrier();
-  if (wr) { if (T > 2) issue(2); seg_barrier(); }
-  // one M + V segment pair per tile j (stage j % 4 a compile-time constant: the loop is unrolled by the ring depth)
-  auto pair = [&](int j, auto CUR) -> bool {
-    constexpr int cur = decltype(CUR)::value;
-    const char* buf = smem + cur * SB;
-    if (j < T) sdp_read(buf);
-    __builtin_amdgcn_sched_barrier(0);
-    if (j >= 1) dvdk_mma();
-    if (j < T) sdp_mma();
-    if (wr && j + 1 < T) retire(j + 2 < T);                  // tile j + 1 landed before the next segment reads it
-    seg_barrier();
-    if (j == T) return false;
-    softmax(buf);
-    if (wr && j + 3 < T) issue(j + 3);
-    seg_barrier();
-    return true;
-  };
-  for (int j = 0;; j += PP_NS) {
-    if (!pair(j, std::integral_constant<int, 0>{})) break;
-    if (!pair(j + 1, std::integral_constant<int, 1>{})) break;
-    if (!pair(j + 2, std::integral_constant<int, 2>{})) break;
-    if (!pair(j + 3, std::integral_constant<int, 3>{})) break;
-  }
-  if (!wr) seg_barrier();                                    // re-align the halves
-  // ---- the halves' partial dK / dV: the leading half finishes dK, the lagging half dV
-  wait_vmcnt<0>();
-  char* slot = smem + kg * 16384;
-  if (wr) pp_put(slot, dk, lane);                            // hand over the half this wave does not finish
-  else pp_put(slot + 8192, dv, lane);                        // (branches, not a selected array: no scratch)
-  lds_barrier();
-  if (!wr) pp_add(slot, dk, lane); else pp_add(slot + 8192, dv, lane);
-  if (sink.dqkv) {
-    float cs[2] = {0.f, 0.f};
-    if (!wr) qkv_sink32<bf16>(sink, 1, b, hh, H, k0, N, lane, dk, -LN2, cs);
-    else {
-      qkv_sink32<bf16>(sink, 2, b, hh, H, k0, N, lane, dv, 1.f, cs);
-      if (sink.ws) qkv_colsum32(sink, 2, hh, H, (blockIdx.y * gridDim.x + blockIdx.x) % S3OD_NREP, lane, cs);
-    }
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const int key = k0 + acc_row(i, h);
-    if (key >= N) continue;
-    if (wr) {
-      bf16* row = dV + ((long)bh * N + key) * 64;
-#pragma unroll
-      for (int db = 0; db < 2; db++) row[32 * db + (lane & 31)] = (bf16)dv[db][i];
-    } else {
-      bf16* row = dK + ((long)bh * N + key) * 64;
-#pragma unroll
-      for (int db = 0; db < 2; db++) row[32 * db + (lane & 31)] = (bf16)(dk[db][i] * -LN2);
-    }
-  }
-}
-
-// dQ.  Workgroup = 128 queries of one (b,h) = 4 query groups of 32; wave w and w + 4 hold the group's Q / dO
-// fragments (negated) and LSE / delta C blocks, and split each 64-key tile into halves.
-__global__ void __launch_bounds__(512) attn_bwd_dq_pp_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
-                                                           const bf16* __restrict__ V, const bf16* __restrict__ dO,
-                                                           const float* __restrict__ LSE, const float* __restrict__ Dl,
-                                                           bf16* __restrict__ dQ, int N, int H, QkvSink sink) {
-  constexpr int SB = 2 * Img32::BYTES;                        // K image, V image
-  static_assert(PP_NS * SB >= 4 * 8192, "dq pp: exchange fits the ring");
-  __shared__ __attribute__((aligned(1024))) char smem[PP_NS * SB];
-  int xb, bh;
-  pp_block(xb, bh);
-  const int b = bh / H, hh = bh - b * H;
-  const int lane = threadIdx.x & 63, wave = pp_wave(), wr = wave >> 2, kg = wave & 3, h = lane >> 5;
-  const char* kbase = (const char*)(K + (long)bh * N * 64);
-  const char* vbase = (const char*)(V + (long)bh * N * 64);
-  const unsigned long tot = (unsigned long)N * 128;
-  Dma64R<4> dkv;
-  dkv.init(128, kg, lane);
-  const int q0 = xb * 128 + kg * 32;
-  bf16x8 qf[4], of[4];
-  f32x16 cl, cd;
-  {
-    const int q = q0 + (lane & 31);
-    const bf16* qr = Q + ((long)bh * N + q) * 64 + 8 * h;
-    const bf16* orow = dO + ((long)b * N + q) * (H * 64) + hh * 64 + 8 * h;
-    bf16x8 z; for (int e = 0; e < 8; e++) z[e] = (bf16)0.f;
-#pragma unroll
-    for (int ks = 0; ks < 4; ks++) {
-      qf[ks] = q < N ? neg8(*(const bf16x8*)(qr + 16 * ks)) : z;
-      of[ks] = q < N ? neg8(*(const bf16x8*)(orow + 16 * ks)) : z;
-    }
-    const float l = q < N ? LSE[(long)bh * N + q] : INFINITY, d = q < N ? Dl[(long)bh * N + q] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; i++) { cl[i] = l; cd[i] = d; }
-  }
-  f32x16 dq[2];
-#pragma unroll
-  for (int db = 0; db < 2; db++) for (int i = 0; i < 16; i++) dq[db][i] = 0.f;
-  const int T = (N + 63) / 64;
-  auto issue = [&](int t) {
-    char* base = smem + (t % PP_NS) * SB;
-    dkv.issue(kbase, tot, (long)t * 64, 128, base, kg);
-    dkv.issue(vbase, tot, (long)t * 64, 128, base + Img32::BYTES, kg);
-  };
-  auto retire = [&](bool keep) { if (keep) wait_vmcnt<4>(); else wait_vmcnt<0>(); };
-  const int kh = 32 * wr;                                    // this wave's key rows in every tile
-  f32x16 s, dp;
-  bf16x8 da[2];              // -dS^T of the pending tile (A operand of dQ)
-  bf16x8 bk[2][2];           // K of the pending tile, transposed (B operand of dQ), read in its V segment
-  bf16x8 ra[4], rc[4];       // K / V rows of the current tile (A operands of S^T / dP^T)
-  auto sdp_read = [&](const char* ks_) {
-    const char* vs_ = ks_ + Img32::BYTES;
-#pragma unroll
-    for (int ks = 0; ks < 4; ks++) { ra[ks] = row32(ks_, kh, ks, lane); rc[ks] = row32(vs_, kh, ks, lane); }
-  };
-  auto sdp_mma = [&]() {
-    s = mma32(ra[0], qf[0], cl);
-    dp = mma32(rc[0], of[0], cd);
-#pragma unroll
-    for (int ks = 1; ks < 4; ks++) { s = mma32(ra[ks], qf[ks], s); dp = mma32(rc[ks], of[ks], dp); }
-  };
-  auto dqk_mma = [&]() {
-#pragma unroll
-    for (int st = 0; st < 2; st++)
-#pragma unroll
-      for (int db = 0; db < 2; db++) dq[db] = mma32(da[st], bk[st][db], dq[db]);
-  };
-  auto softmax = [&](int j, const char* ks_) {  // s = LSE - S^T, dp = delta - dP^T:  -dS^T = exp2(-s) * dp
-#pragma unroll
-    for (int i = 0; i < 16; i++) dp[i] *= fexp2(-s[i]);
-    if (j * 64 + 64 > N) {     // last tile: zero dS of keys >= N (exp2(-lse) may overflow)
-#pragma unroll
-      for (int i = 0; i < 16; i++)
-        if (j * 64 + kh + acc_row(i, h) >= N) dp[i] = 0.f;
-    }
-#pragma unroll
-    for (int st = 0; st < 2; st++) da[st] = pack_acc(dp, st);
-#pragma unroll
-    for (int st = 0; st < 2; st++)
-#pragma unroll
-      for (int db = 0; db < 2; db++) bk[st][db] = tr32(ks_, kh + 16 * st, 32 * db, lane);
-    asm volatile("" ::"v"(da[0]), "v"(da[1]));
-  };
-  if (wr) { issue(0); if (T > 1) issue(1); retire(T > 1); }
-  seg_barrier();
-  if (wr) { if (T > 2) issue(2); seg_barrier(); }
-  auto pair = [&](int j, auto CUR) -> bool {
-    constexpr int cur = decltype(CUR)::value;
-    const char* buf = smem + cur * SB;
-    if (j < T) sdp_read(buf);
-    __builtin_amdgcn_sched_barrier(0);
-    if (j >= 1) dqk_mma();
-    if (j < T) sdp_mma();
-    if (wr && j + 1 < T) retire(j + 2 < T);
-    seg_barrier();
-    if (j == T) return false;
-    softmax(j, buf);
-    if (wr && j + 3 < T) issue(j + 3);
-    seg_barrier();
-    return true;
-  };
-  for (int j = 0;; j += PP_NS) {
-    if (!pair(j, std::integral_constant<int, 0>{})) break;
-    if (!pair(j + 1, std::integral_constant<int, 1>{})) break;
-    if (!pair(j + 2, std::integral_constant<int, 2>{})) break;
-    if (!pair(j + 3, std::integral_constant<int, 3>{})) break;
-  }
-  if (!wr) seg_barrier();
-  wait_vmcnt<0>();
-  char* slot = smem + kg * 8192;
-  if (wr) pp_put(slot, dq, lane);
-  lds_barrier();
-  if (wr) return;
-  pp_add(slot, dq, lane);
-  if (sink.dqkv) {
-    float csq[2] = {0.f, 0.f};
-    qkv_sink32<bf16>(sink, 0, b, hh, H, q0, N, lane, dq, -0.125f, csq);
-    if (sink.ws) qkv_colsum32(sink, 0, hh, H, (blockIdx.y * gridDim.x + blockIdx.x) % S3OD_NREP, lane, csq);
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const int q = q0 + acc_row(i, h);
-    if (q >= N) continue;
-    bf16* r = dQ + ((long)bh * N + q) * 64;
-#pragma unroll
-    for (int db = 0; db < 2; db++) r[32 * db + (lane & 31)] = (bf16)(-dq[db][i]);
-  }
-}
-
 // (hipcc 7.2 left the host stubs of these instances undefined when they were only named in the launcher below)
 template __global__ void attn_bwd_dq32_kernel<4, false, false, true>(const bf16*, const bf16*, const bf16*, const bf16*, const float*,
                                                                      const float*, bf16*, int, int, QkvSink);
@@ -1572,13 +1242,6 @@ void launch_bwd(const void* q, const void* k, const void* v, const void* o, cons
   if constexpr (std::is_same<T, bf16>::value) {
     // bf16: the 32x32x16 kernels, 4 waves per workgroup, tile loops unrolled by two (the 16x16x32 bf16 bodies,
     // 8-wave workgroups, s_setprio and interleaved variants were measured slower and removed: DESIGN §6)
-    if (!S3OD_OFF("S3OD_ATTN_BWD_PP")) {     // the 8-wave ping-pong kernels (S3OD_ATTN_BWD_PP=0: the 4-wave ones, A/B)
-      hipLaunchKernelGGL(attn_bwd_dkdv_pp_kernel, dim3(cdiv(N, 128), B * H), dim3(512), 0, st, (const bf16*)q, (const bf16*)k,
-                         (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv, N, H, sink);
-      hipLaunchKernelGGL(attn_bwd_dq_pp_kernel, dim3(cdiv(N, 128), B * H), dim3(512), 0, st, (const bf16*)q, (const bf16*)k,
-                         (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, N, H, sink);
-      return;
-    }
     hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<4, false, false, true>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st,
                        (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv, N, H,
                        sink);

@@ -131,13 +131,6 @@ DEV void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 // s_barrier WITHOUT the vmcnt(0) a __syncthreads() emits: LDS-DMA stays in flight across it
 DEV void raw_barrier() { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); }
 DEV void lds_barrier() { wait_lgkm0(); __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); }
-// a segment boundary of a ping-pong schedule: no instruction moves across it (register-only MFMAs included)
-DEV void seg_barrier() {
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
 
 // Column reductions over many workgroups add into S3OD_NREP replicas of the accumulator
 // (workgroup b -> replica b % S3OD_NREP) and a second pass folds the replicas: fp32/fp64 atomics

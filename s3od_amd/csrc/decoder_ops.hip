@@ -426,15 +426,19 @@ __global__ void bilinear_bwd_kernel(const T* __restrict__ dy, const float* __res
 }
 
 // ---------------------------------------------------------------- pooled IoU head
-// mean over pixels: x [B, HW, C] -> out [B, C] f32 (atomics; out must be zeroed)
+// mean over pixels: x [B, HW, C] -> out [B, C] f32.  Deterministic (the classifier's pooled input feeds pred_iou and,
+// through d_iou, the broadcast gradient of the whole backward: fp32 atomics here made bf16 gradients differ run to
+// run by ~1e-3 after the chain's bf16 roundings amplified the last-bit differences).  Pass 1: block (k, b) sums pixels
+// [k PPB, (k+1) PPB) into part[b][k][C]; pass 2 adds the partials in k order and scales.
+constexpr int AVGPOOL_PPB = 1024;
 template <typename T>
-__global__ void __launch_bounds__(256) avgpool_kernel(const T* __restrict__ x, float* __restrict__ out, int HW, int C, int pix_per_block) {
+__global__ void __launch_bounds__(256) avgpool_part_kernel(const T* __restrict__ x, float* __restrict__ part, int HW, int C) {
   __shared__ float red[256 * 8];
   const int cg = C / 8, rows = 256 / cg;
   const int t = threadIdx.x, cgi = t % cg, ri = t / cg;
   const int b = blockIdx.y, c = cgi * 8;
   float s[1][8] = {{0, 0, 0, 0, 0, 0, 0, 0}};
-  long p0 = (long)blockIdx.x * pix_per_block, p1 = min((long)HW, p0 + pix_per_block);
+  long p0 = (long)blockIdx.x * AVGPOOL_PPB, p1 = min((long)HW, p0 + AVGPOOL_PPB);
 #pragma unroll 4
   for (long p = p0 + ri; p < p1; p += rows) {
     float v[8]; load8<T>(x + ((long)b * HW + p) * C + c, v);
@@ -443,10 +447,17 @@ __global__ void __launch_bounds__(256) avgpool_kernel(const T* __restrict__ x, f
   }
   rowphase_reduce<1>(s, red, t, cg);
   if (t < cg) {
-    float inv = 1.0f / (float)HW;
+    float* dst = part + ((long)b * gridDim.x + blockIdx.x) * C + c;
 #pragma unroll
-    for (int e = 0; e < 8; e++) atomicAdd(out + (long)b * C + c + e, s[0][e] * inv);
+    for (int e = 0; e < 8; e++) dst[e] = s[0][e];
   }
+}
+__global__ void avgpool_fold_kernel(const float* __restrict__ part, float* __restrict__ out, int nk, int C, float inv) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over B * C
+  const int b = i / C, c = i - b * C;
+  float s = 0.f;
+  for (int k = 0; k < nk; k++) s += part[((long)b * nk + k) * C + c];
+  out[i] = s * inv;
 }
 
 // classifier_head (src/s3od/model.py:185-191): Linear(256,64) -> ReLU -> Linear(64,NM); one block per image
@@ -656,14 +667,15 @@ int s3od_bilinear_bwd(int dtype, const void* dy, const float* bcast, void* dx, i
   return s3od_check_launch("bilinear_bwd");
 }
 
-int s3od_avgpool(int dtype, const void* x, float* out, int B, int HW, int C, void* stream) {
-  S3OD_REQUIRE(C % 8 == 0 && 256 % (C / 8) == 0, "avgpool: C");
+// ws: fp32 [B][ceil(HW / 1024)][C] partial sums (caller-owned, contents dead between calls)
+int s3od_avgpool(int dtype, const void* x, float* out, float* ws, int B, int HW, int C, void* stream) {
+  S3OD_REQUIRE(C % 8 == 0 && 256 % (C / 8) == 0 && (B * C) % 64 == 0 && ws, "avgpool: C / workspace");
   hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(out, 0, sizeof(float) * B * C, st);
-  const int ppb = 1024;
+  const int nk = cdiv(HW, AVGPOOL_PPB);
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(avgpool_kernel<T>, dim3(cdiv(HW, ppb), B), dim3(256), 0, st, (const T*)x, out, HW, C, ppb);
+    hipLaunchKernelGGL(avgpool_part_kernel<T>, dim3(nk, B), dim3(256), 0, st, (const T*)x, ws, HW, C);
   });
+  hipLaunchKernelGGL(avgpool_fold_kernel, dim3(B * C / 64), dim3(64), 0, st, ws, out, nk, C, 1.0f / (float)HW);
   return s3od_check_launch("avgpool");
 }
 

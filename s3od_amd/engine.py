@@ -400,10 +400,9 @@ class DPTEngine:
         # the 4x outputs sum to 4 (edge rows / columns included: clamped taps add up to the same 2 per axis), so
         # mean(up2(c)) = mean(c) exactly in real arithmetic, read from a 4x smaller tensor (C5: 2.2 -> 0.55 GB)
         pooled = torch.empty((B, 256), dtype=torch.float32, device=dev)
-        if os.environ.get("S3OD_POOL_PRE", "1") != "0":     # (A/B: 0 = pool p1 itself)
-            L("s3od_avgpool", dt, c1[0], pooled, B, dims[0][0] * dims[0][1], 256, st)
-        else:
-            L("s3od_avgpool", dt, p1, pooled, B, H1 * W1, 256, st)
+        src, hw = (c1[0], dims[0][0] * dims[0][1]) if os.environ.get("S3OD_POOL_PRE", "1") != "0" else (p1, H1 * W1)
+        part = torch.empty((B, -(-hw // 1024), 256), dtype=torch.float32, device=dev)   # per-1024-pixel partial sums
+        L("s3od_avgpool", dt, src, pooled, part, B, hw, 256, st)
         hid = torch.empty((B, 64), dtype=torch.float32, device=dev)
         nm = self.nm
         iou = torch.empty((B, nm), dtype=torch.float32, device=dev)

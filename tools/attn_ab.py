@@ -79,4 +79,5 @@ if __name__ == "__main__":
     knob, vals = sys.argv[1], sys.argv[2:]
     rounds = int(os.environ.get("AB_ROUNDS", 5))
     run(16, 4101, knob, vals, rounds)
-    run(4, 16389, knob, vals, rounds)
+    if not os.environ.get("AB_SMALL"):
+        run(4, 16389, knob, vals, rounds)

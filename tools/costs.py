@@ -80,7 +80,7 @@ def cost(name, a):
         dt, npix, C = a[0], a[13], a[14]
         return "hbm", npix * C * _t(dt) * 3
     if n == "avgpool":
-        dt, B, HW, C = a[0], a[3], a[4], a[5]
+        dt, B, HW, C = a[0], a[4], a[5], a[6]
         return "hbm", B * HW * C * _t(dt)
     if n == "mask_heads_bwd":
         dt, B, HW = a[0], a[8], a[9]

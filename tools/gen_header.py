@@ -74,6 +74,7 @@ WS = {
     "s3od_qkv_unrope": "ws: fp32 [S3OD_NREP][2][64 H], all zero on entry, left all zero",
     "s3od_attn_bwd_qkv": "ws: fp32 [S3OD_NREP][2][64 H], all zero on entry, left all zero",
     "s3od_conv_wgrad": "ws (nullable): fp32 [Cout][KH][KW][Cin], all zero on entry, left all zero; slab (nullable): >= s3od_conv_wgrad_ws bytes, contents dead between calls",
+    "s3od_avgpool": "ws: fp32 [B][ceil(HW / 1024)][C] partial sums, contents dead between calls (a fixed-order two-pass mean: deterministic)",
     "s3od_linear_wgrad": "slab (nullable): >= s3od_linear_wgrad_ws bytes, contents dead between calls (without it the split-K partials are fp32 atomics into dw)",
 }
 
