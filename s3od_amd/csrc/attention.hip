@@ -96,8 +96,8 @@ DEV float xsum4(float v) { v += __shfl_xor(v, 16); return v + __shfl_xor(v, 32);
 }  // namespace
 
 template <typename T>
-__global__ void __launch_bounds__(256) attn_fwd_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
-                                                        T* __restrict__ O, float* __restrict__ LSE, int N, int H) {
+__global__ void __launch_bounds__(256, 3) attn_fwd_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
+                                                        T* __restrict__ O, float* __restrict__ LSE, int N, int H, int fast) {
   constexpr bool F32 = std::is_same<T, float>::value;
   typedef TileL<T> L;
   __shared__ __attribute__((aligned(16))) char smem[4 * L::BYTES];
@@ -125,12 +125,21 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const T* __restrict__ Q, 
     }
   }
   f32x4 o[4][2];
+  // running max m (log2 units); bf16: C operand -m of the S MFMA, row sums in lacc (MFMA)
+  float mrow[2], lrow[2];
+  f32x4 negm[2], lacc[2];
+  // FAST (bf16): the max is taken over the first key tile only and never moved again -- P = exp2(s - m0) has the
+  // floating-point range of bf16 / fp32, so no per-tile max / threshold VALU is needed (one v_exp + the packing per
+  // score).  A score more than ~120 log2 units above m0 would overflow: the row sum then comes out non-finite and the
+  // workgroup reruns its block with the lazy-rescale loop (FAST = false) before the epilogue.  l >= 1 always (the
+  // maximum of tile 0 contributes exp2(0)), so nothing underflows.
+  auto run = [&](auto FASTc) {
+  constexpr bool FAST = decltype(FASTc)::value;
 #pragma unroll
   for (int i = 0; i < 4; i++) { o[i][0] = f32x4{0, 0, 0, 0}; o[i][1] = f32x4{0, 0, 0, 0}; }
-  // running max m (log2 units); bf16: C operand -m of the S MFMA, row sums in lacc (MFMA)
-  float mrow[2] = {-INFINITY, -INFINITY}, lrow[2] = {0.f, 0.f};
-  f32x4 negm[2] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
-  f32x4 lacc[2] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
+  mrow[0] = mrow[1] = -INFINITY; lrow[0] = lrow[1] = 0.f;
+  negm[0] = negm[1] = f32x4{0, 0, 0, 0};
+  lacc[0] = lacc[1] = f32x4{0, 0, 0, 0};
 
   Stage<T> stg;
   const int nkt = (N + 63) / 64;
@@ -207,9 +216,12 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const T* __restrict__ Q, 
     } else {
       // ---- lazy max: s already holds score - m.  The first tile sets m exactly; later tiles only
       // rescale when a score exceeds m by more than RESCALE_TH (wave-uniform branch).
-      f32x4 c0[4] = {s[0][0], s[1][0], s[2][0], s[3][0]}, c1[4] = {s[0][1], s[1][1], s[2][1], s[3][1]};
-      float lm0 = max16(c0), lm1 = max16(c1);
-      if (kt == 0 || __any(fmaxf(lm0, lm1) > RESCALE_TH)) {
+      float lm0 = 0.f, lm1 = 0.f;
+      if (!FAST || kt == 0) {
+        f32x4 c0[4] = {s[0][0], s[1][0], s[2][0], s[3][0]}, c1[4] = {s[0][1], s[1][1], s[2][1], s[3][1]};
+        lm0 = max16(c0); lm1 = max16(c1);
+      }
+      if (kt == 0 || (!FAST && __any(fmaxf(lm0, lm1) > RESCALE_TH))) {
         float lmq[2] = {lm0, lm1};
 #pragma unroll
         for (int qs = 0; qs < 2; qs++) {
@@ -258,6 +270,19 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const T* __restrict__ Q, 
     if (more) stg.store(smem + (cur ^ 1) * 2 * L::BYTES, smem + (cur ^ 1) * 2 * L::BYTES + L::BYTES, tid);
     __syncthreads();
     cur ^= 1;
+  }
+  };
+  if constexpr (!F32) {
+    if (fast) {
+      run(std::true_type{});
+      // the rare overflow of the fixed-max path: rerun the block with the lazy rescale
+      const bool bad = !(lacc[0][0] < 3.0e38f) || !(lacc[1][0] < 3.0e38f);
+      if (__syncthreads_or(bad)) run(std::false_type{});
+    } else {
+      run(std::false_type{});
+    }
+  } else {
+    run(std::false_type{});
   }
   if constexpr (!F32) { lrow[0] = lacc[0][0]; lrow[1] = lacc[1][0]; }
   // ---- epilogue: O[b][t][h*64 + d], d = ds*16 + 4g + i ; LSE (log2 units) = m + log2(l)
@@ -1217,7 +1242,8 @@ int s3od_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* 
   // bf16 and f32: the 16x16 kernel (a 32x32x16 bf16 variant measured 6-8 % slower: 1083 -> 1150 us at bs 16, N 4101;
   // 3532 -> 3817 us at bs 4, N 16389, same box -- its extra row-sum MFMAs cost 2x the cycles; removed)
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(attn_fwd_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, N, H);
+    hipLaunchKernelGGL(attn_fwd_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, N, H,
+                       S3OD_KNOB("S3OD_ATTN_FAST", 1));   // 0: the lazy-rescale loop throughout (A/B)
   });
   return s3od_check_launch("attn_fwd");
 }

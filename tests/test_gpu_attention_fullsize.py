@@ -139,3 +139,33 @@ def test_attn_bwd_qkv_fused_equals_separate_path():
     assert float((af - ff).norm() / af.norm()) < 4e-3
     for x, y in ((bq_a, bq_f), (bv_a, bv_f)):
         assert float((x - y).abs().max() / x.abs().max()) < 1e-2
+
+
+def test_attention_fwd_fixed_max_overflow_falls_back():
+    """The bf16 forward takes the row max over the first 64 keys only (S3OD_ATTN_FAST): a key whose score exceeds it by
+    more than the fp32 exponent range (here ~290 log2 units) overflows that pass, and the workgroup must rerun the block
+    with the lazy-rescale loop.  Output and LSE vs fp32 softmax, the planted row included."""
+    from s3od_amd._lib import lib, stream, BF16
+    B, H, N = 1, 2, 1000
+    g = torch.Generator(device="cuda").manual_seed(21)
+    q = torch.randn(B * H, N, 64, device="cuda", generator=g)
+    k = torch.randn(B * H, N, 64, device="cuda", generator=g)
+    v = torch.randn(B * H, N, 64, device="cuda", generator=g)
+    q[:, 5] = 0.0
+    q[:, 5, 0] = 40.0            # query 5 of every head ...
+    k[:, 700] = 0.0
+    k[:, 700, 0] = 40.0          # ... meets key 700 (tile 10) with score 40 * 40 / 8 = 200 (natural units)
+    q, k, v = q.bfloat16(), k.bfloat16(), v.bfloat16()
+    qs = (q.float() * (LOG2E * 0.125)).bfloat16()
+    o = torch.empty(B, N, H * 64, dtype=torch.bfloat16, device="cuda")
+    lse2 = torch.empty(B * H, N, device="cuda")
+    lib()("s3od_attn_fwd", BF16, qs, k, v, o, lse2, B, H, N, stream())
+    torch.cuda.synchronize()
+    q_eff = qs.float() / (LOG2E * 0.125)
+    s = torch.matmul(q_eff, k.float().transpose(1, 2)) * 0.125
+    ref = torch.matmul(torch.softmax(s, -1), v.float())
+    got = o.view(B, N, H, 64).permute(0, 2, 1, 3).reshape(B * H, N, 64).float()
+    assert torch.isfinite(got).all() and torch.isfinite(lse2).all()
+    assert float((got - ref).norm() / ref.norm()) < 1e-2
+    assert float((got[:, 5] - ref[:, 5]).abs().max()) < 2e-2          # the planted row: ~ v[700]
+    assert float((lse2 / LOG2E - torch.logsumexp(s, -1)).abs().max()) < 2e-2
