@@ -20,6 +20,11 @@ build/attention.o: $(CSRC)/attention.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(FLAGS) $(ATTN_FLAGS) -c $< -o $@
 
+# the LDS-DMA 3x3 weight gradient keeps its MFMA accumulators in AGPRs (no VGPR form; see the file header)
+build/wgrad_dma.o: $(CSRC)/wgrad_dma.hip $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(filter-out -mllvm -amdgpu-mfma-vgpr-form=1,$(FLAGS)) -c $< -o $@
+
 build/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(FLAGS) -c $< -o $@

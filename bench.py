@@ -357,11 +357,16 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=3, help="timed CPU-baseline iterations (after 1 warm-up)")
     ap.add_argument("--no-infer", action="store_true", help="skip the secondary inference lines (train mode)")
     ap.add_argument("--no-breakdown", action="store_true", help="skip the per-class profiling pass")
+    ap.add_argument("--single-stream", action="store_true",
+                    help="profiling only: the whole run with the backward on one stream (S3OD_BWD_SIDE=0), so rocprofv3 "
+                         "kernel durations are not stretched by the side-stream weight gradients sharing the CUs")
     ap.add_argument("--ddp", action="store_true",
                     help="use the RCCL data-parallel path even at world size 1 (rehearsal on one GPU)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch path only: spawn / join the ranks over gloo (no GPU call), rank 0 reports the world")
     args = ap.parse_args()
+    if args.single_stream:
+        os.environ["S3OD_BWD_SIDE"] = "0"
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
@@ -429,7 +434,8 @@ def main():
         try:
             dom, bd = breakdown(step, 2, peak)
         finally:
-            os.environ.pop("S3OD_BWD_SIDE", None)
+            if not args.single_stream:
+                os.environ.pop("S3OD_BWD_SIDE", None)
         bd["note"] = ("per-entry GPU times from a separate 2-step pass with the encoder backward on one stream (the timed "
                       "region runs the weight gradients on a side stream beside the data-gradient chain)")
     torch.cuda.synchronize()

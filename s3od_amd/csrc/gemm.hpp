@@ -122,6 +122,12 @@ struct DmaSink {
 };
 #define HD __host__ __device__
 
+// 8 x 32-pixel output tiles of the 3x3 halo weight-gradient kernels (gemm_ops.hip, wgrad_dma.hip)
+constexpr int HT_TH = 8, HT_TW = 32, HT_HR = HT_TH + 2, HT_HC = HT_TW + 2, HT_PX = HT_HR * HT_HC;
+// LDS-DMA 3x3 weight gradient, 64 x 64 channel blocks (wgrad_dma.hip; needs H % 8 == 0, W % 32 == 0)
+int wgrad3x3_dma_launch(bool relu_x, const bf16* dy, const bf16* x, float* ws, int B, int H, int W, int CinT, int CoT,
+                        hipStream_t st);
+
 template <int RB> DEV int mc_logical_byte(int k, int phys) {
   constexpr int SLOTS = RB / 32;
   int g = ((k & 3) | (((k >> 3) & 1) << 2)) & (SLOTS - 1);

@@ -166,8 +166,6 @@ template <typename T> struct EpiHeads {
   }
 };
 
-// 8 x 32-pixel output tiles of the halo weight-gradient kernels below
-constexpr int HT_TH = 8, HT_TW = 32, HT_HR = HT_TH + 2, HT_HC = HT_TW + 2, HT_PX = HT_HR * HT_HC;
 
 // ---------------------------------------------------------------- register-weight 3x3 conv, 64 -> 64
 // The full-resolution 64-channel convs (upsample_2x.2 forward and its stride-1 data gradient) move
@@ -922,103 +920,6 @@ static int launch_wgrad_halo(const bf16* dy, const bf16* x, float* ws, int B, in
   return s3od_check_launch("conv3x3_wgrad_halo");
 }
 
-// LDS-DMA form of the 64-channel-block halo wgrad (Cout block 64): the dy tile (256 px x 64) and the x halo
-// (10 x 34 px x 64) of the NEXT tile land by buffer_load ... lds into the other half of a 2-deep ring while this
-// tile's MFMAs run, so there is no register staging (PT x 4 VGPRs), no ds_write and one barrier per tile.  The
-// DMA lanes pick the global 16-B chunk that the XOR swizzle (dy_at / hx_at) puts at their LDS position.
-namespace wgd {
-constexpr int DYB = 256 * 128, HXB = HT_PX * 128, PIECES = 76, PPW = PIECES / 4, BUF = PIECES * 1024, LDS = 2 * BUF;
-static_assert(DYB % 1024 == 0 && DYB + HXB <= BUF && LDS <= 160 * 1024, "wgrad dma layout");
-}  // namespace wgd
-template <bool RELU>
-__global__ void __launch_bounds__(256, 1)
-conv3x3_wgrad_dma_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, float* __restrict__ ws, int H, int W,
-                         int tiles_x, int tiles_y, int ntiles, int CinT, int CoT, int nci, int wpc) {
-  using namespace wgd;
-  constexpr int NCO = 4, NP = 9;
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
-  // channel block of this workgroup and its contiguous tile range (as in the register-staged kernel; an XCD-grouped
-  // order that runs the channel blocks of one tile behind one L2 measured the same)
-  const int combo = blockIdx.x / wpc, wi = blockIdx.x - combo * wpc;
-  const int t_beg = (int)((long)ntiles * wi / wpc), t_end = (int)((long)ntiles * (wi + 1) / wpc);
-  const int co0 = (combo / nci) * 64, ci0 = (combo % nci) * 64;
-  const int pair0 = NP * wave;
-  f32x4 acc[NP][NCO];
-#pragma unroll
-  for (int i = 0; i < NP; i++)
-#pragma unroll
-    for (int j = 0; j < NCO; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // piece p = PPW wave + i: bytes [1024 p, +1024) of a ring slot; pieces < 32 = dy image [256 px][128 B],
-  // the rest = halo image [340 px][128 B] (beyond it: dummy).  dm = (row y << 16) | (col x << 4) | logical chunk
-  int dm[PPW];
-#pragma unroll
-  for (int i = 0; i < PPW; i++) {
-    const int p = wave * PPW + i, b = p * 1024 + lane * 16;
-    if (p < DYB / 1024) {
-      const int row = b >> 7, c = ((b >> 4) & 7) ^ (row & 7);
-      dm[i] = ((row / HT_TW) << 16) | ((row % HT_TW) << 4) | c;
-    } else {
-      const int hb = b - DYB, row = hb >> 7, c = ((hb >> 4) & 7) ^ (row & 7);
-      dm[i] = row < HT_PX ? ((row / HT_HC) << 16) | ((row % HT_HC) << 4) | c : -1;
-    }
-  }
-  auto issue = [&](int tile, int slot) {
-    const int txi = tile % tiles_x, t2 = tile / tiles_x, tyi = t2 % tiles_y, b = t2 / tiles_y;
-    const int ty0 = tyi * HT_TH, tx0 = txi * HT_TW;
-    const long img_d = (long)H * W * CoT, img_x = (long)H * W * CinT;
-    const auto rd = make_rsrc(dy + b * img_d, (unsigned long)img_d * 2);
-    const auto rx = make_rsrc(x + b * img_x, (unsigned long)img_x * 2);
-    char* dst = smem + slot * BUF + wave * PPW * 1024;
-#pragma unroll
-    for (int i = 0; i < PPW; i++) {
-      const int p = wave * PPW + i, v = dm[i];
-      if (p < DYB / 1024) {                              // wave-uniform
-        const int gy = ty0 + (v >> 16), gx = tx0 + ((v >> 4) & 0xfff);
-        const bool ok = gy < H && gx < W;
-        blds16(rd, ok ? (unsigned)(((gy * W + gx) * CoT + co0) * 2 + (v & 15) * 16) : 0x80000000u, dst + i * 1024);
-      } else {
-        const int gy = ty0 - 1 + (v >> 16), gx = tx0 - 1 + ((v >> 4) & 0xfff);
-        const bool ok = v >= 0 && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
-        blds16(rx, ok ? (unsigned)(((gy * W + gx) * CinT + ci0) * 2 + (v & 15) * 16) : 0x80000000u, dst + i * 1024);
-      }
-    }
-  };
-  int tile = t_beg, k = 0;
-  if (tile < t_end) issue(tile, 0);
-  for (; tile < t_end; tile++, k++) {
-    wait_vmcnt<0>();                                     // this tile's pieces (the only vector-memory ops in flight)
-    __builtin_amdgcn_s_barrier();                        // ... of every wave; every wave done with the other slot
-    asm volatile("" ::: "memory");
-    if (tile + 1 < t_end) issue(tile + 1, (k + 1) & 1);
-    const char* dyi = smem + (k & 1) * BUF;
-    const char* hxi = dyi + DYB;
-    for (int ty = 0; ty < HT_TH; ty++) {                  // K step = one output row of 32 pixels
-      bf16x8 fa[NCO];
-#pragma unroll
-      for (int cb = 0; cb < NCO; cb++) fa[cb] = trf(dyi, ty * HT_TW, cb * 16, lane, dy_at<64>);
-#pragma unroll
-      for (int j = 0; j < NP; j++) {
-        const int pr = pair0 + j, tap = pr >> 2, cib = pr & 3, tdy = tap / 3, tdx = tap - tdy * 3;
-        bf16x8 fb = trf(hxi, (ty + tdy) * HT_HC + tdx, cib * 16, lane, hx_at);
-        if constexpr (RELU) fb = __builtin_bit_cast(bf16x8, relu16<bf16>(__builtin_bit_cast(uint4, fb)));
-#pragma unroll
-        for (int cb = 0; cb < NCO; cb++) acc[j][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[cb], fb, acc[j][cb], 0, 0, 0);
-      }
-    }
-  }
-  const int g = lane >> 4, li = lane & 15;
-#pragma unroll
-  for (int j = 0; j < NP; j++) {
-    const int pr = pair0 + j, tap = pr >> 2, cib = pr & 3;
-#pragma unroll
-    for (int cb = 0; cb < NCO; cb++)
-#pragma unroll
-      for (int r = 0; r < 4; r++)
-        atomicAdd(ws + (long)(co0 + cb * 16 + 4 * g + r) * (9 * CinT) + tap * CinT + ci0 + cib * 16 + li, acc[j][cb][r]);
-  }
-}
-
 // Weight gradient of the 4x4 / stride-2 / pad-1 conv view of upsample_2x.0 (ConvTranspose2d(128, 64, 4, 2, 1)):
 // dW[co][ky][kx][ci] = sum_p dy[p][co] * x[2p - 1 + (ky, kx)][ci], dy on the OH x OW grid (128 channels), x on the
 // 2OH x 2OW grid (64).  The same LDS-DMA / register-accumulator scheme as the 3x3 kernel above with 16 taps:
@@ -1128,20 +1029,6 @@ static int launch_wgrad4s2(const bf16* dy, const bf16* x, float* ws, int B, int 
   const int wpc = (int)std::max<long>(1, std::min<long>(tiles, std::max(1, s3od_cu_count() / nblk)));
   hipLaunchKernelGGL(kfn, dim3(nblk * wpc), dim3(256), wg4::LDS, st, dy, x, ws, OH, OW, tx, ty, (int)tiles, CinT, CoT, nci, wpc);
   return s3od_check_launch("conv4s2_wgrad_dma");
-}
-
-// S3OD_WGRAD_DMA=0 (under S3OD_AB=1: per call) keeps the register-staged kernel
-template <bool RELU>
-static int launch_wgrad_dma(const bf16* dy, const bf16* x, float* ws, int B, int H, int W, int CinT, int CoT, hipStream_t st) {
-  auto kfn = conv3x3_wgrad_dma_kernel<RELU>;
-  static const bool attr = ((void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, wgd::LDS), true);   // once per process (thread-safe static init)
-  (void)attr;
-  const int tx = cdiv(W, HT_TW), ty = cdiv(H, HT_TH);
-  const long tiles = (long)B * tx * ty;
-    const int nci = CinT / 64, nblk = (CoT / 64) * nci;
-  const int wpc = (int)std::max<long>(1, std::min<long>(tiles, std::max(1, s3od_cu_count() / nblk)));
-  hipLaunchKernelGGL(kfn, dim3(nblk * wpc), dim3(256), wgd::LDS, st, dy, x, ws, H, W, tx, ty, (int)tiles, CinT, CoT, nci, wpc);
-  return s3od_check_launch("conv3x3_wgrad_dma");
 }
 
 template <int BM, int BN> struct Tile {};
@@ -1710,9 +1597,9 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
   const int coblk = Cout % 64 == 0 ? 64 : (Cout == 96 ? 96 : 0);
   if (wg_knob && dtype == S3OD_BF16 && ws && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W &&
       Cin % 64 == 0 && coblk && (Cin == 64 || (long)H * W >= 512L * 512)) {
-    const bool dma = coblk == 64 && (long)H * W * (Cin > Cout ? Cin : Cout) * 2 < (1L << 31) && !S3OD_OFF("S3OD_WGRAD_DMA");
-    int rc = dma ? (relu_x ? launch_wgrad_dma<true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)
-                           : launch_wgrad_dma<false>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)) :
+    const bool dma = coblk == 64 && (long)H * W * (Cin > Cout ? Cin : Cout) * 2 < (1L << 31) && H % HT_TH == 0 && W % HT_TW == 0 &&
+                     !S3OD_OFF("S3OD_WGRAD_DMA");
+    int rc = dma ? wgrad3x3_dma_launch(relu_x, (const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st) :
              coblk == 64 ? (relu_x ? launch_wgrad_halo<64, true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)
                                    : launch_wgrad_halo<64, false>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st))
                          : (relu_x ? launch_wgrad_halo<96, true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)

@@ -84,10 +84,13 @@ def test_mask_heads_fwd_halo():
     _close(hsave.view(B, H, W, 32 * NM), _nhwc(h))
 
 
-@pytest.mark.parametrize("cout,B,H,W,relu", [(64, 2, 37, 45, False), (96, 1, 40, 70, False), (64, 3, 16, 33, True)])
+@pytest.mark.parametrize("cout,B,H,W,relu", [(64, 2, 37, 45, False), (96, 1, 40, 70, False), (64, 3, 16, 33, True),
+                                             (64, 2, 64, 96, False), (64, 3, 16, 64, True), (64, 1, 8, 32, True)])
 def test_conv_wgrad_halo(cout, B, H, W, relu):
     """3x3 s1 weight gradient (halo-tile kernel for Cin 64 -> Cout 64 / 96) vs torch's conv2d_weight of
-    the same bf16 operands, accumulated into an existing gradient (+=)."""
+    the same bf16 operands, accumulated into an existing gradient (+=).  H % 8 == 0 and W % 32 == 0 with Cout 64
+    take the LDS-DMA kernel (csrc/wgrad_dma.hip: every border case, one-tile images, several images per workgroup);
+    the ragged shapes the register-staged one."""
     from s3od_amd._lib import lib, stream
     g = torch.Generator(device="cuda").manual_seed(cout + H)
     dy = torch.randn(B, cout, H, W, device="cuda", generator=g).bfloat16()
@@ -105,7 +108,7 @@ def test_conv_wgrad_halo(cout, B, H, W, relu):
 
 
 @pytest.mark.parametrize("cin,cout,B,H,W,relu", [(256, 256, 2, 20, 36, True), (128, 192, 1, 512, 520, True),
-                                                  (256, 128, 1, 520, 512, False)])
+                                                  (256, 128, 1, 520, 512, False), (128, 128, 2, 512, 512, True)])
 def test_conv_wgrad_halo_channel_blocks(cin, cout, B, H, W, relu):
     """The halo wgrad over 64-channel blocks of wider convs (used from 512^2 maps: the output_conv1 shape;
     smaller maps take the implicit GEMM, checked by the first case)."""

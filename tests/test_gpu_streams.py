@@ -46,7 +46,7 @@ def test_side_stream_backward_equals_single_stream_f32():
     a, b = _grads(True, dt="f32"), _grads(False, dt="f32")
     for rep in (0, 1):
         assert a[rep].keys() == b[rep].keys()
-        worst = (0.0, None)
+        worst = (0.0, "")
         for n in a[rep]:
             if _skip(n):
                 continue

@@ -2,7 +2,8 @@
 (S3OD_WGRAD_DMA=0, read per call), one process, interleaved rounds; results compared (dev tool).
 Shapes: upsample_2x.2 (1024^2, 64 -> 64) and output_conv1 (512^2, 256 -> 128, ReLU'd input).
 
-    python tools/wgrad_bench.py
+    python tools/wgrad_bench.py            # A/B, every shape
+    python tools/wgrad_bench.py pmc        # DMA kernel only, 1024^2 64 -> 64 and 512^2 256 -> 128, one round (profiling)
 """
 import os
 os.environ.setdefault("S3OD_AB", "1")   # knobs toggled per call (csrc/common.hpp S3OD_KNOB)
@@ -29,15 +30,16 @@ def timeit(fn, n=5):
 
 def main():
     B = 16
-    for (H, cin, cout, relu) in ((1024, 64, 64, 0), (512, 256, 128, 0), (512, 256, 128, 1)):
+    pmc = sys.argv[1:] == ["pmc"]
+    for (H, cin, cout, relu) in ((1024, 64, 64, 0), (512, 256, 128, 0)) + (() if pmc else ((512, 256, 128, 1),)):
         g = torch.Generator(device="cuda").manual_seed(H + cin)
         dy = torch.randn(B, H, H, cout, device="cuda", generator=g).bfloat16()
         x = torch.randn(B, H, H, cin, device="cuda", generator=g).bfloat16()
         ws = torch.zeros(cout * 9 * cin, device="cuda")
         fl = 2.0 * B * H * H * cin * cout * 9
         res = {}
-        for rnd in range(3):
-            for knob in ("0", "1"):
+        for rnd in range(1 if pmc else 3):
+            for knob in ("1",) if pmc else ("0", "1"):
                 os.environ["S3OD_WGRAD_DMA"] = knob
                 dw = torch.zeros(cout, cin, 3, 3, device="cuda")
                 f = lambda: lib()("s3od_conv_wgrad", BF16, B, H, H, cin, H, H, cout, 3, 3, 1, 1, dy, x, relu, dw, ws, 0, None, 0, stream())
@@ -47,10 +49,14 @@ def main():
                 torch.cuda.synchronize()
                 res[knob] = dw.clone()
                 print(f"{H}^2 {cin}->{cout} relu {relu} round {rnd} DMA={knob}: {t * 1e6:8.1f} us {fl / t / 1e12:7.1f} TF/s", flush=True)
+        if pmc:
+            continue
         b = res["0"]
         for k in ("1",):
             a = res[k]
             print(f"{H}^2 {k}: max |dma - staged| / max|staged| = {float((a - b).abs().max() / b.abs().max()):.3e}")
+    if pmc:
+        return
     # upsample_2x.0 (ConvTranspose2d(128, 64, 4, 2, 1)) in its conv view: dy 512^2 x 128, x 1024^2 x 64
     H = 512
     g = torch.Generator(device="cuda").manual_seed(7)
