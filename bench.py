@@ -510,6 +510,13 @@ def main():
             "mfma_frac_step": round(value / world * per_img / peak, 4) if per_img else None,
             "finite": ok,
         }
+        if bd and dom in bd["by_entry"] and bd["by_entry"][dom].get("calls_per_step"):
+            # the same entry in the single-stream breakdown pass: what a single-stream rocprofv3 trace of the step
+            # (profiles/<tag>_ss_summary.md) reports for its kernels, without the side stream's CU sharing
+            e = bd["by_entry"][dom]
+            ms1 = e["ms_per_step"] / e["calls_per_step"]
+            res["roofline"]["single_stream"] = {"mean_launch_ms": round(ms1, 4), "frac": e.get("frac_of_peak", e.get("frac_of_hbm")),
+                                                "source": "breakdown pass (S3OD_BWD_SIDE=0), HIP events per call"}
         if dom.startswith("s3od_attn_bwd") and kms > 0:
             # what the kernels issue: S recomputed in the dK/dV pass, S and dP again in the dQ pass
             ex = work * 14.0 / 8.0

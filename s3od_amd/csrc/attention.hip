@@ -896,21 +896,9 @@ typedef __attribute__((address_space(3))) void lds_void;
 DEV __amdgpu_buffer_rsrc_t attn_rsrc(const void* p, unsigned long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(unsigned)bytes, 0x00020000);
 }
-template <int W> struct Dma64 {
-  static constexpr int NIW = 8 / W;
-  // stage rows row0 .. row0+63 (row stride ldb bytes) of buffer r into the image at `img`
-  DEV static void issue(__amdgpu_buffer_rsrc_t r, long row0, long ldb, char* img, int wave, int lane) {
-#pragma unroll
-    for (int i = 0; i < NIW; i++) {
-      const int o = (wave * NIW + i) * 1024 + lane * 16, row = o >> 7, lc = ((o >> 4) & 7) ^ Img32::sw(row);
-      const long src = (row0 + row) * ldb + lc * 16;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(img + (wave * NIW + i) * 1024), 16,
-                                               src < 0x7FFFFFFFL ? (unsigned)src : 0x80000000u, 0, 0, 0);
-    }
-  }
-};
-// The same with the descriptor rebased on the tile's first row (scalar work only): the per-lane source offsets are
-// loop-invariant registers, so a tile's DMA issue costs no vector ALU.  `total` = the buffer's byte size from `base`;
+// Stage rows row0 .. row0+63 (row stride ldb bytes) into the image, the descriptor rebased on the tile's first row
+// (scalar work only): the per-lane source offsets are loop-invariant registers, so a tile's DMA issue costs no
+// vector ALU.  `total` = the buffer's byte size from `base`;
 // rows past its end still read zeros (range check against the rebased size).
 template <int W> struct Dma64R {
   static constexpr int NIW = 8 / W;
@@ -934,9 +922,6 @@ template <int W> struct Dma64R {
 DEV void dma_row64r(const float* base, int N, int q0, unsigned vo, char* dst) {   // vo = lane < 16 ? 16 lane : OOB
   __builtin_amdgcn_raw_ptr_buffer_load_lds(attn_rsrc(base + q0, (unsigned long)(N - q0) * 4), (lds_void*)dst, 16, vo, 0, 0, 0);
 }
-DEV void dma_row64(__amdgpu_buffer_rsrc_t r, long q0, char* dst, int lane) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, lane < 16 ? (unsigned)((q0 + 4 * lane) * 4) : 0x80000000u, 0, 0, 0);
-}
 DEV f32x16 ld16(const float* p) {      // 4 consecutive-row groups of the 32x32 C layout (rows 8m + 0..3)
   const f32x4 a = *(const f32x4*)(p), b = *(const f32x4*)(p + 8), c = *(const f32x4*)(p + 16), d = *(const f32x4*)(p + 24);
   return f32x16{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3], c[0], c[1], c[2], c[3], d[0], d[1], d[2], d[3]};
@@ -953,9 +938,8 @@ DEV bf16x8 neg8(bf16x8 v) {
 // and value fragments are held negated, so the accumulators start at +LSE / +delta straight from LDS and hold
 // LSE - S and delta - dP (exp2 takes the negation for free as an input modifier); dS is carried negated and
 // flipped at the store.
-// PRIO: the second half of the workgroup's waves run at s_setprio 1 (MI355X_MICROARCH "Two waves per SIMD" item 4)
-// IL: interleave the softmax VALU of one 32-query half between the other half's MFMAs (sched_group_barrier)
-template <int W, bool PRIO, bool IL, bool U2 = false>
+// (s_setprio halves and sched_group_barrier-interleaved softmax variants were measured slower and removed: DESIGN §6)
+template <int W>
 __global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                                    const bf16* __restrict__ V, const bf16* __restrict__ dO,
                                                                    const float* __restrict__ LSE, const float* __restrict__ Dl,
@@ -966,15 +950,11 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __r
   const int bh = blockIdx.y, b = bh / H, hh = bh - b * H;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5;
   const long ldo = (long)H * 64;
-  const auto rq = attn_rsrc(Q + (long)bh * N * 64, (unsigned long)N * 128);
-  const auto rdo = attn_rsrc(dO + (long)b * N * ldo + hh * 64, ((unsigned long)(N - 1) * ldo + 64) * 2);
-  const auto rl = attn_rsrc(LSE + (long)bh * N, (unsigned long)N * 4);
-  const auto rd = attn_rsrc(Dl + (long)bh * N, (unsigned long)N * 4);
   Dma64R<W> dq_, ddo;
-  if constexpr (U2) { dq_.init(128, wave, lane); ddo.init(ldo * 2, wave, lane); }
+  dq_.init(128, wave, lane);
+  ddo.init(ldo * 2, wave, lane);
   const unsigned vrow = lane < 16 ? 16u * lane : 0x80000000u;
   const int k0 = blockIdx.x * (32 * W) + wave * 32;
-  if (PRIO && wave >= W / 2) __builtin_amdgcn_s_setprio(1);
   bf16x8 kf[4], vf[4];
   {
     const int key = k0 + (lane & 31);
@@ -992,25 +972,18 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __r
   for (int db = 0; db < 2; db++) for (int i = 0; i < 16; i++) { dk[db][i] = 0.f; dv[db][i] = 0.f; }
   const int nqt = (N + 63) / 64;
   auto stage = [&](int qt, char* base) {
-    if constexpr (U2) {
-      dq_.issue((const char*)(Q + (long)bh * N * 64), (unsigned long)N * 128, (long)qt * 64, 128, base, wave);
-      ddo.issue((const char*)(dO + (long)b * N * ldo + hh * 64), ((unsigned long)(N - 1) * ldo + 64) * 2, (long)qt * 64, ldo * 2,
-                base + Img32::BYTES, wave);
-      if (wave == 0) dma_row64r(LSE + (long)bh * N, N, qt * 64, vrow, base + 2 * Img32::BYTES);
-      if (wave == W - 1) dma_row64r(Dl + (long)bh * N, N, qt * 64, vrow, base + 2 * Img32::BYTES + 1024);
-    } else {
-      Dma64<W>::issue(rq, (long)qt * 64, 128, base, wave, lane);
-      Dma64<W>::issue(rdo, (long)qt * 64, ldo * 2, base + Img32::BYTES, wave, lane);
-      if (wave == 0) dma_row64(rl, (long)qt * 64, base + 2 * Img32::BYTES, lane);
-      if (wave == W - 1) dma_row64(rd, (long)qt * 64, base + 2 * Img32::BYTES + 1024, lane);
-    }
+    dq_.issue((const char*)(Q + (long)bh * N * 64), (unsigned long)N * 128, (long)qt * 64, 128, base, wave);
+    ddo.issue((const char*)(dO + (long)b * N * ldo + hh * 64), ((unsigned long)(N - 1) * ldo + 64) * 2, (long)qt * 64, ldo * 2,
+              base + Img32::BYTES, wave);
+    if (wave == 0) dma_row64r(LSE + (long)bh * N, N, qt * 64, vrow, base + 2 * Img32::BYTES);
+    if (wave == W - 1) dma_row64r(Dl + (long)bh * N, N, qt * 64, vrow, base + 2 * Img32::BYTES + 1024);
   };
   stage(0, smem);
   __syncthreads();
-  // U2: the tile loop unrolled by two so the LDS stage is a compile-time constant (every fragment address
+  // the tile loop is unrolled by two so the LDS stage is a compile-time constant (every fragment address
   // becomes a per-lane base + immediate instead of being recomputed from the stage index each tile)
   auto tile = [&](int qt, auto CUR) {
-    const int cur = CUR;     // std::integral_constant (U2) or the runtime stage index
+    constexpr int cur = decltype(CUR)::value;
     if (qt + 1 < nqt) stage(qt + 1, smem + (cur ^ 1) * SB);
     const char* qs_ = smem + cur * SB;
     const char* dos = qs_ + Img32::BYTES;
@@ -1050,34 +1023,20 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __r
         for (int db = 0; db < 2; db++) { dv[db] = mma32(pa[qb][st], bo[db], dv[db]); dk[db] = mma32(da[qb][st], bq[db], dk[db]); }
       }
     };
-    auto interleave = [&]() {      // 8 MFMAs, each followed by up to 6 VALU (the other half's softmax)
-#pragma unroll
-      for (int g = 0; g < 8; g++) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
-      }
-    };
     sdp(0);
     __builtin_amdgcn_sched_barrier(0);
     sdp(1);
     softmax(0);
-    if (IL) interleave();
     __builtin_amdgcn_sched_barrier(0);
     dvdk(0);
     softmax(1);
-    if (IL) interleave();
     __builtin_amdgcn_sched_barrier(0);
     dvdk(1);
     __syncthreads();      // drains this tile's reads and the next tile's LDS-DMA (vmcnt(0)) before the flip
   };
-  if constexpr (U2) {
-    int qt = 0;
-    for (; qt + 1 < nqt; qt += 2) { tile(qt, std::integral_constant<int, 0>{}); tile(qt + 1, std::integral_constant<int, 1>{}); }
-    if (qt < nqt) tile(qt, std::integral_constant<int, 0>{});
-  } else {
-    int cur = 0;
-    for (int qt = 0; qt < nqt; qt++) { tile(qt, cur); cur ^= 1; }
-  }
+  int qt = 0;
+  for (; qt + 1 < nqt; qt += 2) { tile(qt, std::integral_constant<int, 0>{}); tile(qt + 1, std::integral_constant<int, 1>{}); }
+  if (qt < nqt) tile(qt, std::integral_constant<int, 0>{});
   if (sink.dqkv) {
     float csk[2] = {0.f, 0.f}, csv[2] = {0.f, 0.f};
     qkv_sink32<bf16>(sink, 1, b, hh, H, k0, N, lane, dk, -LN2, csk);
@@ -1101,7 +1060,7 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __r
 
 // dQ (w.r.t. the pre-scaled q).  Workgroup = W waves x 32 queries; loop over 64-key tiles (K, V by LDS-DMA).
 // Same sign convention: Q and dO fragments negated, C = +LSE / +delta of the lane's query (constant blocks).
-template <int W, bool PRIO, bool IL, bool U2 = false>
+template <int W>
 __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __restrict__ Q, const bf16* __restrict__ K,
                                                                  const bf16* __restrict__ V, const bf16* __restrict__ dO,
                                                                  const float* __restrict__ LSE, const float* __restrict__ Dl,
@@ -1110,12 +1069,9 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __res
   __shared__ __attribute__((aligned(1024))) char smem[2 * SB];
   const int bh = blockIdx.y, b = bh / H, hh = bh - b * H;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5;
-  const auto rk = attn_rsrc(K + (long)bh * N * 64, (unsigned long)N * 128);
-  const auto rv = attn_rsrc(V + (long)bh * N * 64, (unsigned long)N * 128);
   Dma64R<W> dkv;
-  if constexpr (U2) dkv.init(128, wave, lane);
+  dkv.init(128, wave, lane);
   const int q0 = blockIdx.x * (32 * W) + wave * 32;
-  if (PRIO && wave >= W / 2) __builtin_amdgcn_s_setprio(1);
   bf16x8 qf[4], of[4];
   f32x16 cl, cd;     // C operands: LSE (log2 units) / delta of the lane's query, all 16 rows
   {
@@ -1137,18 +1093,13 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __res
   for (int db = 0; db < 2; db++) for (int i = 0; i < 16; i++) dq[db][i] = 0.f;
   const int nkt = (N + 63) / 64;
   auto stage = [&](int kt, char* base) {
-    if constexpr (U2) {
-      dkv.issue((const char*)(K + (long)bh * N * 64), (unsigned long)N * 128, (long)kt * 64, 128, base, wave);
-      dkv.issue((const char*)(V + (long)bh * N * 64), (unsigned long)N * 128, (long)kt * 64, 128, base + Img32::BYTES, wave);
-    } else {
-      Dma64<W>::issue(rk, (long)kt * 64, 128, base, wave, lane);
-      Dma64<W>::issue(rv, (long)kt * 64, 128, base + Img32::BYTES, wave, lane);
-    }
+    dkv.issue((const char*)(K + (long)bh * N * 64), (unsigned long)N * 128, (long)kt * 64, 128, base, wave);
+    dkv.issue((const char*)(V + (long)bh * N * 64), (unsigned long)N * 128, (long)kt * 64, 128, base + Img32::BYTES, wave);
   };
   stage(0, smem);
   __syncthreads();
-  auto tile = [&](int kt, auto CUR) {      // U2: as in the dK/dV pass
-    const int cur = CUR;
+  auto tile = [&](int kt, auto CUR) {      // unrolled by two, as in the dK/dV pass
+    constexpr int cur = decltype(CUR)::value;
     if (kt + 1 < nkt) stage(kt + 1, smem + (cur ^ 1) * SB);
     const char* ks_ = smem + cur * SB;
     const char* vs_ = ks_ + Img32::BYTES;
@@ -1185,33 +1136,20 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __res
         for (int db = 0; db < 2; db++) dq[db] = mma32(da[kb][st], bk[db], dq[db]);
       }
     };
-    auto interleave = [&](int n) {
-      for (int g = 0; g < n; g++) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
-      }
-    };
     sdp(0);
     __builtin_amdgcn_sched_barrier(0);
     sdp(1);
     softmax(0);
-    if (IL) interleave(8);
     __builtin_amdgcn_sched_barrier(0);
     dqk(0);
     softmax(1);
-    if (IL) interleave(4);
     __builtin_amdgcn_sched_barrier(0);
     dqk(1);
     __syncthreads();
   };
-  if constexpr (U2) {
-    int kt = 0;
-    for (; kt + 1 < nkt; kt += 2) { tile(kt, std::integral_constant<int, 0>{}); tile(kt + 1, std::integral_constant<int, 1>{}); }
-    if (kt < nkt) tile(kt, std::integral_constant<int, 0>{});
-  } else {
-    int cur = 0;
-    for (int kt = 0; kt < nkt; kt++) { tile(kt, cur); cur ^= 1; }
-  }
+  int kt = 0;
+  for (; kt + 1 < nkt; kt += 2) { tile(kt, std::integral_constant<int, 0>{}); tile(kt + 1, std::integral_constant<int, 1>{}); }
+  if (kt < nkt) tile(kt, std::integral_constant<int, 0>{});
   if (sink.dqkv) {
     float csq[2] = {0.f, 0.f};
     qkv_sink32<bf16>(sink, 0, b, hh, H, q0, N, lane, dq, -0.125f, csq);
@@ -1229,10 +1167,10 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __res
 }
 
 // (hipcc 7.2 left the host stubs of these instances undefined when they were only named in the launcher below)
-template __global__ void attn_bwd_dq32_kernel<4, false, false, true>(const bf16*, const bf16*, const bf16*, const bf16*, const float*,
-                                                                     const float*, bf16*, int, int, QkvSink);
-template __global__ void attn_bwd_dkdv32_kernel<4, false, false, true>(const bf16*, const bf16*, const bf16*, const bf16*, const float*,
-                                                                       const float*, bf16*, bf16*, int, int, QkvSink);
+template __global__ void attn_bwd_dq32_kernel<4>(const bf16*, const bf16*, const bf16*, const bf16*, const float*, const float*, bf16*,
+                                                 int, int, QkvSink);
+template __global__ void attn_bwd_dkdv32_kernel<4>(const bf16*, const bf16*, const bf16*, const bf16*, const float*, const float*, bf16*,
+                                                   bf16*, int, int, QkvSink);
 
 extern "C" {
 
@@ -1268,10 +1206,10 @@ void launch_bwd(const void* q, const void* k, const void* v, const void* o, cons
   if constexpr (std::is_same<T, bf16>::value) {
     // bf16: the 32x32x16 kernels, 4 waves per workgroup, tile loops unrolled by two (the 16x16x32 bf16 bodies,
     // 8-wave workgroups, s_setprio and interleaved variants were measured slower and removed: DESIGN §6)
-    hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<4, false, false, true>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st,
+    hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<4>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st,
                        (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dk, (bf16*)dv, N, H,
                        sink);
-    hipLaunchKernelGGL((attn_bwd_dq32_kernel<4, false, false, true>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st,
+    hipLaunchKernelGGL((attn_bwd_dq32_kernel<4>), dim3(cdiv(N, 128), B * H), dim3(256), 0, st,
                        (const bf16*)q, (const bf16*)k, (const bf16*)v, (const bf16*)dout, lse, delta, (bf16*)dq, N, H, sink);
     return;
   } else {

@@ -17,6 +17,7 @@ static_assert(DYB % 1024 == 0 && DYB + HXB <= BUF && LDS <= 160 * 1024, "wgrad d
 }  // namespace wgd
 // Transposed 16 x 32 fragment (rows = K) at a precomputed per-lane LDS address (lo rows) + 2048 (hi rows, 16 rows on)
 typedef __attribute__((address_space(3))) char lds_char;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 DEV bf16x8 trf_at(const lds_char* a) {
   typedef __attribute__((address_space(3))) s16x4 lds4;
   s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)a);
@@ -152,16 +153,160 @@ conv3x3_wgrad_dma_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x
         atomicAdd(ws + (long)(co0 + cb * 16 + 4 * g + r) * (9 * CinT) + t * CinT + ci0 + wave * 16 + li, acc[t][cb][r]);
 }
 
+// Producer-wave form: waves 0..3 compute exactly as above and never touch vector memory; NPROD more waves issue the
+// 76 DMA pieces of the next tile (piece j by producer j % NPROD).  In the 4-wave kernel every compute wave issues
+// 19 pieces at the top of each tile and stalls at issue once the memory queue is full (1.4 us of a 5.5 us tile at
+// 1024^2, measured with wall_clock64 stamps), and compute alone (800 us) + DMA alone (786 us) ran in 1215 us together.
+// The producers absorb the issue stalls; the compute waves only meet them at the one barrier per tile.  A second
+// wave on a SIMD caps every wave at 256 registers (144 AGPR accumulators + <= 112 VGPRs).
+template <bool RELU, int NPROD>
+__global__ void __launch_bounds__(64 * (4 + NPROD), 1)
+conv3x3_wgrad_dmap_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, float* __restrict__ ws, int H, int W,
+                          int tiles_x, int tiles_y, int ntiles, int CinT, int CoT, int nci, int wpc) {
+  using namespace wgd;
+  constexpr int NCO = 4, NP = 9, DP = DYB / 1024, HP = PIECES - DP;    // 32 dy + 44 halo pieces
+  constexpr int DPP = DP / NPROD, HPP = HP / NPROD;                    // per producer
+  static_assert(HP * 8 >= HT_PX && DP % NPROD == 0 && HP % NPROD == 0, "wgrad dma pieces");
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int combo = blockIdx.x / wpc, wi = blockIdx.x - combo * wpc;
+  const int t_beg = (int)((long)ntiles * wi / wpc), t_end = (int)((long)ntiles * (wi + 1) / wpc);
+  const int co0 = (combo / nci) * 64, ci0 = (combo % nci) * 64;
+  if (wave >= 4) {
+    // the piece layout of the 4-wave kernel; producer pw takes dy pieces pw + NPROD i and halo pieces pw + NPROD j
+    const int pw = wave - 4;
+    const int l8 = lane >> 3, ch = (lane & 7) ^ l8;
+    const unsigned dlo = (unsigned)(l8 * CoT * 2 + ch * 16);
+    unsigned hlo[HPP], hcode[(HPP + 7) / 8];
+#pragma unroll
+    for (int j = 0; j < (HPP + 7) / 8; j++) hcode[j] = 0u;
+#pragma unroll
+    for (int j = 0; j < HPP; j++) {
+      const int row = (pw + NPROD * j) * 8 + l8, hy = row / HT_HC, hx = row - hy * HT_HC;
+      hlo[j] = row < HT_PX ? (unsigned)(((hy * W + hx) * CinT) * 2 + ch * 16) : 0x80000000u;
+      const unsigned code = (hy == 0 ? 1u : 0u) | (hy == HT_HR - 1 ? 2u : 0u) | (hx == 0 ? 4u : 0u) | (hx == HT_HC - 1 ? 8u : 0u);
+      hcode[j / 8] |= code << (4 * (j % 8));
+    }
+    auto issue = [&](int tile, int slot) __attribute__((always_inline)) {
+      const int txi = tile % tiles_x, t2 = tile / tiles_x, tyi = t2 % tiles_y, b = t2 / tiles_y;
+      const int ty0 = tyi * HT_TH, tx0 = txi * HT_TW;
+      const long img_d = (long)H * W * CoT, img_x = (long)H * W * CinT;
+      const long od = ((long)ty0 * W + tx0) * CoT + co0, ox = ((long)(ty0 - 1) * W + tx0 - 1) * CinT + ci0;
+      const auto rd = make_rsrc(dy + b * img_d + od, (unsigned long)(img_d - od) * 2);
+      const auto rx = make_rsrc(x + b * img_x + ox, (unsigned long)(img_x - ox) * 2);
+      char* dd = smem + slot * BUF;
+      char* hd = smem + slot * BUF + DYB;
+      const unsigned m = (ty0 == 0 ? 1u : 0u) | (ty0 + HT_TH == H ? 2u : 0u) | (tx0 == 0 ? 4u : 0u) | (tx0 + HT_TW == W ? 8u : 0u);
+      // halo pieces first: under a ReLU'd input the producers rectify the halo while the dy pieces still land
+#pragma unroll
+      for (int j = 0; j < HPP; j++)
+        blds16(rx, ((hcode[j / 8] >> (4 * (j % 8))) & m) ? 0x80000000u : hlo[j], hd + (pw + NPROD * j) * 1024);
+#pragma unroll
+      for (int j = 0; j < DPP; j++) {
+        const int p = pw + NPROD * j;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rd, (lds_void*)(dd + p * 1024), 16, dlo, ((p >> 2) * W + 8 * (p & 3)) * CoT * 2, 0, 0);
+      }
+    };
+    if (t_beg < t_end) issue(t_beg, 0);
+    for (int tile = t_beg, k = 0; tile < t_end; tile++, k++) {
+      if (RELU) {
+        wait_vmcnt<DPP>();                               // the halo pieces landed (the dy pieces are the younger DPP)
+        // ReLU'd input: the producers rectify the landed halo in place (the compute waves read it unchanged; a
+        // v_pk_max per fragment read there cost 384 VALU per 576 MFMAs and spilled)
+        // every 16-B chunk of the slot's halo region, dummy tail included (HP KiB = NPROD x 64 lanes x NIT chunks),
+        // in inline asm: compiled LDS accesses here get a conservative vmcnt(0) in front (the dy DMA still in flight
+        // may alias for the compiler) and an lgkmcnt(0) each, which serialised the pass
+        constexpr int STEP = 64 * NPROD, NIT = HP * 64 / STEP;
+        static_assert(NIT * STEP == HP * 64 && NIT * STEP * 16 <= 65536, "relu pass layout");
+        const unsigned a0 = (unsigned)(size_t)(const lds_char*)(smem + (k & 1) * BUF + DYB) + (pw * 64 + lane) * 16;
+        u32x4 v[NIT];
+#pragma unroll
+        for (int i = 0; i < NIT; i++) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v[i]) : "v"(a0), "n"(i * STEP * 16));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < NIT; i++)
+#pragma unroll
+          for (int e = 0; e < 4; e++) asm volatile("v_pk_max_i16 %0, %0, 0" : "+v"(v[i][e]));
+#pragma unroll
+        for (int i = 0; i < NIT; i++) asm volatile("ds_write_b128 %0, %1 offset:%2" :: "v"(a0), "v"(v[i]), "n"(i * STEP * 16) : "memory");
+        wait_lgkm0();                                    // the stores are in LDS before the barrier
+      }
+      wait_vmcnt<0>();                                   // tile's pieces landed
+      __builtin_amdgcn_s_barrier();                      // pairs with the compute waves' barrier of this tile
+      asm volatile("" ::: "memory");
+      if (tile + 1 < t_end) issue(tile + 1, (k + 1) & 1);
+    }
+    return;
+  }
+  f32x4 acc[NP][NCO];
+#pragma unroll
+  for (int i = 0; i < NP; i++)
+#pragma unroll
+    for (int j = 0; j < NCO; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int u = 4 * (lane >> 4) + ((lane & 15) >> 2), pq = lane & 3;
+  const lds_char* sb = (const lds_char*)smem;
+  unsigned fab[2][4], hxb[2][8];
+#pragma unroll
+  for (int sl = 0; sl < 2; sl++) {
+#pragma unroll
+    for (int cb = 0; cb < 4; cb++)
+      fab[sl][cb] = sl * BUF + u * 128 + 16 * ((2 * cb + (pq >> 1)) ^ (u & 7)) + 8 * (pq & 1);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      hxb[sl][k] = sl * BUF + DYB + u * 128 + 16 * ((2 * wave + (pq >> 1)) ^ ((k + u) & 7)) + 8 * (pq & 1);
+  }
+  // A compiler memory clobber every second row: the two rows of a pair share their halo reads, but fragments are not
+  // kept live across pairs (all-rows reuse needs ~30 live halo fragments: > 112 VGPRs; per-row clobbers: 1062 vs 1000 us
+  // for pairs, opaque per-row bases 1108 us -- v_mov / v_add per fragment -- at 1024^2, same process)
+  auto tile_step = [&](auto SLOT) __attribute__((always_inline)) {
+    constexpr int slot = decltype(SLOT)::value;
+    __syncthreads();                                     // LDS reads of the previous tile done; this tile's data landed
+    asm volatile("" ::: "memory");
+    wgd_row<false, 0>(sb, fab[slot], hxb[slot], acc); wgd_row<false, 1>(sb, fab[slot], hxb[slot], acc);
+    asm volatile("" ::: "memory");
+    wgd_row<false, 2>(sb, fab[slot], hxb[slot], acc); wgd_row<false, 3>(sb, fab[slot], hxb[slot], acc);
+    asm volatile("" ::: "memory");
+    wgd_row<false, 4>(sb, fab[slot], hxb[slot], acc); wgd_row<false, 5>(sb, fab[slot], hxb[slot], acc);
+    asm volatile("" ::: "memory");
+    wgd_row<false, 6>(sb, fab[slot], hxb[slot], acc); wgd_row<false, 7>(sb, fab[slot], hxb[slot], acc);
+  };
+  int tile = t_beg;
+  for (; tile + 1 < t_end; tile += 2) {
+    tile_step(std::integral_constant<int, 0>{});
+    tile_step(std::integral_constant<int, 1>{});
+  }
+  if (tile < t_end) tile_step(std::integral_constant<int, 0>{});
+  const int g = lane >> 4, li = lane & 15;
+#pragma unroll
+  for (int t = 0; t < NP; t++)
+#pragma unroll
+    for (int cb = 0; cb < NCO; cb++)
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        atomicAdd(ws + (long)(co0 + cb * 16 + 4 * g + r) * (9 * CinT) + t * CinT + ci0 + wave * 16 + li, acc[t][cb][r]);
+}
+
+// S3OD_WGD_PROD=0 (under S3OD_AB=1: per call) keeps the 4-wave kernel
 template <bool RELU>
 static int launch_wgrad_dma(const bf16* dy, const bf16* x, float* ws, int B, int H, int W, int CinT, int CoT, hipStream_t st) {
-  auto kfn = conv3x3_wgrad_dma_kernel<RELU>;
-  static const bool attr = ((void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, wgd::LDS), true);   // once per process (thread-safe static init)
+  const bool prod = S3OD_KNOB("S3OD_WGD_PROD", 1) != 0;
+  const int np = S3OD_KNOB("S3OD_WGD_NPROD", 2);
+  auto kp = np == 4 ? conv3x3_wgrad_dmap_kernel<RELU, 4> : np == 2 ? conv3x3_wgrad_dmap_kernel<RELU, 2> : conv3x3_wgrad_dmap_kernel<RELU, 1>;
+  static const bool attr = ((void)hipFuncSetAttribute((const void*)conv3x3_wgrad_dma_kernel<RELU>, hipFuncAttributeMaxDynamicSharedMemorySize, wgd::LDS),
+                            (void)hipFuncSetAttribute((const void*)conv3x3_wgrad_dmap_kernel<RELU, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, wgd::LDS),
+                            (void)hipFuncSetAttribute((const void*)conv3x3_wgrad_dmap_kernel<RELU, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, wgd::LDS),
+                            (void)hipFuncSetAttribute((const void*)conv3x3_wgrad_dmap_kernel<RELU, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, wgd::LDS),
+                            true);   // once per process (thread-safe static init)
   (void)attr;
   const int tx = cdiv(W, HT_TW), ty = cdiv(H, HT_TH);
   const long tiles = (long)B * tx * ty;
-    const int nci = CinT / 64, nblk = (CoT / 64) * nci;
+  const int nci = CinT / 64, nblk = (CoT / 64) * nci;
   const int wpc = (int)std::max<long>(1, std::min<long>(tiles, std::max(1, s3od_cu_count() / nblk)));
-  hipLaunchKernelGGL(kfn, dim3(nblk * wpc), dim3(256), wgd::LDS, st, dy, x, ws, H, W, tx, ty, (int)tiles, CinT, CoT, nci, wpc);
+  if (prod)
+    hipLaunchKernelGGL(kp, dim3(nblk * wpc), dim3(64 * (4 + (np == 4 || np == 2 ? np : 1))), wgd::LDS, st, dy, x, ws, H, W, tx, ty, (int)tiles,
+                       CinT, CoT, nci, wpc);
+  else
+    hipLaunchKernelGGL(conv3x3_wgrad_dma_kernel<RELU>, dim3(nblk * wpc), dim3(256), wgd::LDS, st, dy, x, ws, H, W, tx, ty, (int)tiles, CinT, CoT, nci, wpc);
   return s3od_check_launch("conv3x3_wgrad_dma");
 }
 

@@ -95,6 +95,31 @@ for k, v in per_kernel.items():
 lines.append(f"- traffic per `{entry}` call: {traffic / 1e9:.3f} GB")
 (dst / f"{tag}_summary.md").write_text("\n".join(lines) + "\n")
 
+# ---- the single-stream training pass (S3OD_BWD_SIDE=0): kernel durations without the side stream's CU sharing ----
+ss = src / "trace_train_ss"
+if ss.exists():
+    fs, rs = stats("trace_train_ss")
+    shutil.copy(fs, dst / f"{tag}_ss_kernel_stats.csv")
+    tots = sum(float(r["TotalDurationNs"]) for r in rs)
+    ls = [f"# rocprofv3 kernel stats, SINGLE-STREAM pass, round tag {tag}", "",
+          "Pass: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-infer "
+          "--no-breakdown --single-stream` (configs[2]; the whole backward on one stream, S3OD_BWD_SIDE=0, so no two "
+          "kernels share the CUs and each duration is the kernel's own).  The timed bench line runs the weight "
+          "gradients on a side stream; its roofline.single_stream object is this pass's counterpart (HIP events).",
+          f"Total kernel time {tots / 1e6:.1f} ms over {steps} steps = {tots / 1e6 / steps:.1f} ms/step.", "",
+          "| ms/step | % | calls | avg us | kernel |", "|---:|---:|---:|---:|---|"]
+    for r in rs[:45]:
+        ls.append(f"| {float(r['TotalDurationNs']) / 1e6 / steps:.2f} | {float(r['Percentage']):.2f} | {r['Calls']} | "
+                  f"{float(r['AverageNs']) / 1e3:.1f} | `{r['Name'][:110]}` |")
+    ent = [r for r in rs if kre.search(r["Name"])]
+    if ent:
+        ls += ["", f"Kernels of one `{entry}` call (regex `{kre.pattern}`): " +
+               ", ".join(f"`{r['Name'][:60]}` {float(r['AverageNs']) / 1e3:.1f} us" for r in ent) +
+               f"; sum {sum(float(r['AverageNs']) for r in ent) / 1e3:.1f} us per call."]
+    (dst / f"{tag}_ss_summary.md").write_text("\n".join(ls) + "\n")
+    if (src / "bench_train_ss.json").exists():
+        shutil.copy(src / "bench_train_ss.json", dst / f"{tag}_bench_train_ss.json")
+
 # ---- C5 inference: stats + every kernel's HBM bytes ----
 f5, rows5 = stats("trace_c5")
 shutil.copy(f5, dst / f"{tag}_c5_kernel_stats.csv")

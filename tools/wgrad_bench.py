@@ -1,5 +1,6 @@
-"""A/B of the halo-tile 3x3 weight gradients at bs 16: the LDS-DMA kernel (default) vs the register-staged one
-(S3OD_WGRAD_DMA=0, read per call), one process, interleaved rounds; results compared (dev tool).
+"""A/B of the halo-tile 3x3 weight gradients at bs 16: the LDS-DMA kernel (default: producer-wave form) vs the
+register-staged one (S3OD_WGRAD_DMA=0) and the 4-wave LDS-DMA form (p0 = S3OD_WGD_PROD=0), knobs read per call,
+one process, interleaved rounds; results compared (dev tool).
 Shapes: upsample_2x.2 (1024^2, 64 -> 64) and output_conv1 (512^2, 256 -> 128, ReLU'd input).
 
     python tools/wgrad_bench.py            # A/B, every shape
@@ -30,8 +31,52 @@ def timeit(fn, n=5):
 
 def main():
     B = 16
-    pmc = sys.argv[1:] == ["pmc"]
-    for (H, cin, cout, relu) in ((1024, 64, 64, 0), (512, 256, 128, 0)) + (() if pmc else ((512, 256, 128, 1),)):
+    pmc = sys.argv[1:2] == ["pmc"]
+    if sys.argv[1:2] == ["dbg"]:                  # per-wave wall-clock split of the producer kernel (S3OD_WGD_DBG)
+        H, cin, cout = 1024, 64, 64
+        dy = torch.randn(B, H, H, cout, device="cuda").bfloat16()
+        x = torch.randn(B, H, H, cin, device="cuda").bfloat16()
+        ws = torch.zeros(cout * 9 * cin, device="cuda")
+        dw = torch.zeros(cout, cin, 3, 3, device="cuda")
+        buf = torch.zeros(4096 * 5 * 8, dtype=torch.int64, device="cuda")
+        f = lambda: lib()("s3od_conv_wgrad", BF16, B, H, H, cin, H, H, cout, 3, 3, 1, 1, dy, x, 0, dw, ws, 0, None, 0, stream())
+        if len(sys.argv) > 3:
+            os.environ[sys.argv[2]] = sys.argv[3]
+        t = timeit(f)
+        os.environ["S3OD_WGD_DBG"] = str(buf.data_ptr())
+        f()
+        torch.cuda.synchronize()
+        os.environ.pop("S3OD_WGD_DBG")
+        d = buf.view(-1, 5, 8).cpu().double()
+        d = d[d[:, 0, 5] > 0]
+        n = d[:, 0, 5:6]
+        print(f"{t * 1e6:.1f} us; {len(d)} workgroups, {float(n.mean()):.1f} tiles each (us per tile)")
+        for w in range(5):
+            e = d[:, w] / 100
+            nm = ("compute", "barrier", "-") if w < 4 else ("vmwait", "barrier", "issue")
+            print(f"  wave {w}: {nm[0]} {float((e[:, 0] / n[:, 0]).mean()):.3f} {nm[1]} {float((e[:, 1] / n[:, 0]).mean()):.3f}"
+                  f" {nm[2]} {float((e[:, 2] / n[:, 0]).mean()):.3f}  span {float((e[:, 4] - e[:, 3]).mean()):.1f} us")
+        return
+    if sys.argv[1:2] == ["xp"]:                   # experiment: A/B of a dev knob (argv[2], values argv[3:]) at 1024^2 64 -> 64
+        H, cin, cout = 1024, 64, 64                # (XP_SHAPE=512: 512^2 256 -> 128 with the ReLU'd input)
+        relu = 0
+        if os.environ.get("XP_SHAPE") == "512":
+            H, cin, cout, relu = 512, 256, 128, 1
+        dy = torch.randn(B, H, H, cout, device="cuda").bfloat16()
+        x = torch.randn(B, H, H, cin, device="cuda").bfloat16()
+        ws = torch.zeros(cout * 9 * cin, device="cuda")
+        dw = torch.zeros(cout, cin, 3, 3, device="cuda")
+        for rnd in range(2):
+            for xp in sys.argv[3:]:
+                os.environ[sys.argv[2]] = xp
+                t = timeit(lambda: lib()("s3od_conv_wgrad", BF16, B, H, H, cin, H, H, cout, 3, 3, 1, 1, dy, x, relu, dw, ws, 0, None, 0, stream()))
+                print(f"{sys.argv[2]}={xp}: {t * 1e6:8.1f} us", flush=True)
+        os.environ.pop(sys.argv[2])
+        return
+    shapes = ((1024, 64, 64, 0), (512, 256, 128, 0)) + (() if pmc else ((512, 256, 128, 1),))
+    if sys.argv[1:] == ["pmc", "1024"]:
+        shapes = shapes[:1]
+    for (H, cin, cout, relu) in shapes:
         g = torch.Generator(device="cuda").manual_seed(H + cin)
         dy = torch.randn(B, H, H, cout, device="cuda", generator=g).bfloat16()
         x = torch.randn(B, H, H, cin, device="cuda", generator=g).bfloat16()
@@ -39,8 +84,9 @@ def main():
         fl = 2.0 * B * H * H * cin * cout * 9
         res = {}
         for rnd in range(1 if pmc else 3):
-            for knob in ("1",) if pmc else ("0", "1"):
-                os.environ["S3OD_WGRAD_DMA"] = knob
+            for knob in ("1",) if pmc else ("0", "1", "p0"):
+                os.environ["S3OD_WGRAD_DMA"] = knob[-1]
+                os.environ["S3OD_WGD_PROD"] = "0" if knob == "p0" else "1"
                 dw = torch.zeros(cout, cin, 3, 3, device="cuda")
                 f = lambda: lib()("s3od_conv_wgrad", BF16, B, H, H, cin, H, H, cout, 3, 3, 1, 1, dy, x, relu, dw, ws, 0, None, 0, stream())
                 t = timeit(f)
@@ -52,9 +98,10 @@ def main():
         if pmc:
             continue
         b = res["0"]
-        for k in ("1",):
+        for k in ("1", "p0"):
             a = res[k]
             print(f"{H}^2 {k}: max |dma - staged| / max|staged| = {float((a - b).abs().max() / b.abs().max()):.3e}")
+    os.environ.pop("S3OD_WGD_PROD", None)
     if pmc:
         return
     # upsample_2x.0 (ConvTranspose2d(128, 64, 4, 2, 1)) in its conv view: dy 512^2 x 128, x 1024^2 x 64
