@@ -48,6 +48,11 @@ template <> struct TileL<float> {
   DEV static int vrow(int key, int byte) { return key * 272 + byte; }
 };
 
+typedef __attribute__((address_space(3))) void lds_void;
+DEV __amdgpu_buffer_rsrc_t attn_rsrc(const void* p, unsigned long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(unsigned)bytes, 0x00020000);
+}
+
 template <typename T> struct Stage {
   static constexpr int CH = 64 * 64 * sizeof(T) / 16 / 256;   // 16-B chunks per thread per tile
   uint4 k[CH], v[CH];
@@ -71,6 +76,22 @@ template <typename T> struct Stage {
       k[i] = ok ? *(const uint4*)(K + (long)key * 64 + col) : make_uint4(0, 0, 0, 0);
       v[i] = ok ? *(const uint4*)(V + (long)key * 64 + col) : make_uint4(0, 0, 0, 0);
     }
+  }
+  // bf16: the same chunks by buffer loads -- per-thread byte offsets fixed, the tile's key offset on the scalar unit,
+  // keys >= N read zeros by the range check: no per-tile address or select VALU (the global-pointer form spent ~80
+  // VALU per tile on 64-bit addresses and tail selects beside 36 MFMAs)
+  DEV void load_buf(__amdgpu_buffer_rsrc_t rk, __amdgpu_buffer_rsrc_t rv, const unsigned (&vo)[CH], int key0) {
+    const int so = key0 * 64 * (int)sizeof(T);
+#pragma unroll
+    for (int i = 0; i < CH; i++) {
+      k[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rk, vo[i], so, 0));
+      v[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rv, vo[i], so, 0));
+    }
+  }
+  DEV static unsigned chunk_off(int tid, int i) {
+    constexpr int CPR = 64 * sizeof(T) / 16;
+    const int c = tid + 256 * i;
+    return (unsigned)((c / CPR) * 64 * sizeof(T) + (c % CPR) * 16);
   }
   DEV void store(char* ks, char* vs, int tid) {
 #pragma unroll
@@ -143,13 +164,21 @@ __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(const T* __restrict__ 
 
   Stage<T> stg;
   const int nkt = (N + 63) / 64;
-  stg.load(Kp, Vp, 0, N, tid);
+  const auto rk = attn_rsrc(Kp, (unsigned long)N * 64 * sizeof(T)), rv = attn_rsrc(Vp, (unsigned long)N * 64 * sizeof(T));
+  unsigned vo[Stage<T>::CH];
+#pragma unroll
+  for (int i = 0; i < Stage<T>::CH; i++) vo[i] = Stage<T>::chunk_off(tid, i);
+  auto stage_load = [&](int key0) {
+    if constexpr (F32) stg.load(Kp, Vp, key0, N, tid);
+    else stg.load_buf(rk, rv, vo, key0);
+  };
+  stage_load(0);
   stg.store(smem, smem + L::BYTES, tid);
   __syncthreads();
   int cur = 0;
   for (int kt = 0; kt < nkt; kt++) {
     const bool more = kt + 1 < nkt;
-    if (more) stg.load(Kp, Vp, (kt + 1) * 64, N, tid);
+    if (more) stage_load((kt + 1) * 64);
     const char* ks = smem + cur * 2 * L::BYTES;
     const char* vs = ks + L::BYTES;
     // ---- S^T = K Q^T (- m) : acc[kb][qs], element i: key = kb*16 + 4g + i, query = qs*16 + li
@@ -892,10 +921,6 @@ DEV void qkv_colsum32(const QkvSink& o, int which, int hh, int H, int rep, int l
 // LDS-DMA of a 64-row x 128-B tile into an Img32 (buffer_load_dwordx4 ... lds: one wave instruction fills 1 KiB
 // of LDS lane-linearly, so the image's XOR swizzle is applied to each lane's SOURCE chunk), W waves.  Rows past
 // the buffer's end read zeros (hardware range check), so tile tails need no masking.
-typedef __attribute__((address_space(3))) void lds_void;
-DEV __amdgpu_buffer_rsrc_t attn_rsrc(const void* p, unsigned long bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(unsigned)bytes, 0x00020000);
-}
 // Stage rows row0 .. row0+63 (row stride ldb bytes) into the image, the descriptor rebased on the tile's first row
 // (scalar work only): the per-lane source offsets are loop-invariant registers, so a tile's DMA issue costs no
 // vector ALU.  `total` = the buffer's byte size from `base`;

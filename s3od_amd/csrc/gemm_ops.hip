@@ -1597,8 +1597,11 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
   const int coblk = Cout % 64 == 0 ? 64 : (Cout == 96 ? 96 : 0);
   if (wg_knob && dtype == S3OD_BF16 && ws && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W &&
       Cin % 64 == 0 && coblk && (Cin == 64 || (long)H * W >= 512L * 512)) {
-    const bool dma = coblk == 64 && (long)H * W * (Cin > Cout ? Cin : Cout) * 2 < (1L << 31) && H % HT_TH == 0 && W % HT_TW == 0 &&
-                     !S3OD_OFF("S3OD_WGRAD_DMA");
+    // the LDS-DMA kernel works on 64 x 64 channel blocks; the 96-output-channel mask heads (Cin 64) run as two output
+    // blocks, the second reading 32 channels past each pixel's 96 (finite data of the next pixel, zeros past the image)
+    // whose products are never flushed
+    const bool dma = (coblk == 64 || (coblk == 96 && Cin == 64)) && (long)H * W * (Cin > Cout ? Cin : Cout) * 2 < (1L << 31) &&
+                     H % HT_TH == 0 && W % HT_TW == 0 && !S3OD_OFF("S3OD_WGRAD_DMA");
     int rc = dma ? wgrad3x3_dma_launch(relu_x, (const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st) :
              coblk == 64 ? (relu_x ? launch_wgrad_halo<64, true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)
                                    : launch_wgrad_halo<64, false>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st))

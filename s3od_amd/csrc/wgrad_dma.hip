@@ -150,7 +150,8 @@ conv3x3_wgrad_dma_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x
     for (int cb = 0; cb < NCO; cb++)
 #pragma unroll
       for (int r = 0; r < 4; r++)
-        atomicAdd(ws + (long)(co0 + cb * 16 + 4 * g + r) * (9 * CinT) + t * CinT + ci0 + wave * 16 + li, acc[t][cb][r]);
+        if (co0 + cb * 16 + 4 * g + r < CoT)               // (CoT = 96: the second block's top half is padding)
+          atomicAdd(ws + (long)(co0 + cb * 16 + 4 * g + r) * (9 * CinT) + t * CinT + ci0 + wave * 16 + li, acc[t][cb][r]);
 }
 
 // Producer-wave form: waves 0..3 compute exactly as above and never touch vector memory; NPROD more waves issue the
@@ -283,7 +284,8 @@ conv3x3_wgrad_dmap_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ 
     for (int cb = 0; cb < NCO; cb++)
 #pragma unroll
       for (int r = 0; r < 4; r++)
-        atomicAdd(ws + (long)(co0 + cb * 16 + 4 * g + r) * (9 * CinT) + t * CinT + ci0 + wave * 16 + li, acc[t][cb][r]);
+        if (co0 + cb * 16 + 4 * g + r < CoT)               // (CoT = 96: the second block's top half is padding)
+          atomicAdd(ws + (long)(co0 + cb * 16 + 4 * g + r) * (9 * CinT) + t * CinT + ci0 + wave * 16 + li, acc[t][cb][r]);
 }
 
 // S3OD_WGD_PROD=0 (under S3OD_AB=1: per call) keeps the 4-wave kernel
@@ -300,7 +302,7 @@ static int launch_wgrad_dma(const bf16* dy, const bf16* x, float* ws, int B, int
   (void)attr;
   const int tx = cdiv(W, HT_TW), ty = cdiv(H, HT_TH);
   const long tiles = (long)B * tx * ty;
-  const int nci = CinT / 64, nblk = (CoT / 64) * nci;
+  const int nci = CinT / 64, nblk = cdiv(CoT, 64) * nci;
   const int wpc = (int)std::max<long>(1, std::min<long>(tiles, std::max(1, s3od_cu_count() / nblk)));
   if (prod)
     hipLaunchKernelGGL(kp, dim3(nblk * wpc), dim3(64 * (4 + (np == 4 || np == 2 ? np : 1))), wgd::LDS, st, dy, x, ws, H, W, tx, ty, (int)tiles,

@@ -85,12 +85,13 @@ def test_mask_heads_fwd_halo():
 
 
 @pytest.mark.parametrize("cout,B,H,W,relu", [(64, 2, 37, 45, False), (96, 1, 40, 70, False), (64, 3, 16, 33, True),
-                                             (64, 2, 64, 96, False), (64, 3, 16, 64, True), (64, 1, 8, 32, True)])
+                                             (64, 2, 64, 96, False), (64, 3, 16, 64, True), (64, 1, 8, 32, True),
+                                             (96, 2, 32, 64, True), (96, 1, 8, 32, False)])
 def test_conv_wgrad_halo(cout, B, H, W, relu):
     """3x3 s1 weight gradient (halo-tile kernel for Cin 64 -> Cout 64 / 96) vs torch's conv2d_weight of
     the same bf16 operands, accumulated into an existing gradient (+=).  H % 8 == 0 and W % 32 == 0 with Cout 64
-    take the LDS-DMA kernel (csrc/wgrad_dma.hip: every border case, one-tile images, several images per workgroup);
-    the ragged shapes the register-staged one."""
+    take the LDS-DMA kernel (csrc/wgrad_dma.hip: every border case, one-tile images, several images per workgroup;
+    Cout 96 as two 64-channel blocks, the second padded); the ragged shapes the register-staged one."""
     from s3od_amd._lib import lib, stream
     g = torch.Generator(device="cuda").manual_seed(cout + H)
     dy = torch.randn(B, cout, H, W, device="cuda", generator=g).bfloat16()

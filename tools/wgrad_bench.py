@@ -1,7 +1,7 @@
 """A/B of the halo-tile 3x3 weight gradients at bs 16: the LDS-DMA kernel (default: producer-wave form) vs the
 register-staged one (S3OD_WGRAD_DMA=0) and the 4-wave LDS-DMA form (p0 = S3OD_WGD_PROD=0), knobs read per call,
 one process, interleaved rounds; results compared (dev tool).
-Shapes: upsample_2x.2 (1024^2, 64 -> 64) and output_conv1 (512^2, 256 -> 128, ReLU'd input).
+Shapes: upsample_2x.2 (1024^2, 64 -> 64), output_conv1 (512^2, 256 -> 128, ReLU'd input), mask heads (1024^2, 64 -> 96).
 
     python tools/wgrad_bench.py            # A/B, every shape
     python tools/wgrad_bench.py pmc        # DMA kernel only, 1024^2 64 -> 64 and 512^2 256 -> 128, one round (profiling)
@@ -73,7 +73,7 @@ def main():
                 print(f"{sys.argv[2]}={xp}: {t * 1e6:8.1f} us", flush=True)
         os.environ.pop(sys.argv[2])
         return
-    shapes = ((1024, 64, 64, 0), (512, 256, 128, 0)) + (() if pmc else ((512, 256, 128, 1),))
+    shapes = ((1024, 64, 64, 0), (512, 256, 128, 0)) + (() if pmc else ((512, 256, 128, 1), (1024, 64, 96, 0)))
     if sys.argv[1:] == ["pmc", "1024"]:
         shapes = shapes[:1]
     for (H, cin, cout, relu) in shapes:
