@@ -935,7 +935,7 @@ static_assert(AB % 1024 == 0 && LDS <= 160 * 1024, "wgrad 4s2 layout");
 }  // namespace wg4
 __global__ void __launch_bounds__(256, 1)
 conv4s2_wgrad_dma_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, float* __restrict__ ws, int OH, int OW,
-                         int tiles_x, int tiles_y, int ntiles, int CinT, int CoT, int nci, int wpc) {
+                         int tiles_x, int tiles_y, int ntiles, int CinT, int CoT, int nci, int wpc, int ymaj) {
   using namespace wg4;
   constexpr int NCO = 4, NP = 16;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
@@ -964,7 +964,10 @@ conv4s2_wgrad_dma_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x
     }
   }
   auto issue = [&](int tile, int slot) {
-    const int txi = tile % tiles_x, t2 = tile / tiles_x, tyi = t2 % tiles_y, b = t2 / tiles_y;
+    // ymaj: consecutive tiles walk down a column (the halo's top 2 of 6 rows were the previous tile's: L2)
+    int txi, tyi, b;
+    if (ymaj) { tyi = tile % tiles_y; const int t2 = tile / tiles_y; txi = t2 % tiles_x; b = t2 / tiles_x; }
+    else { txi = tile % tiles_x; const int t2 = tile / tiles_x; tyi = t2 % tiles_y; b = t2 / tiles_y; }
     const int oy0 = tyi * TH, ox0 = txi * TW;
     const long img_d = (long)OH * OW * CoT, img_x = (long)IH * IW * CinT;
     const auto rd = make_rsrc(dy + b * img_d, (unsigned long)img_d * 2);
@@ -1027,7 +1030,8 @@ static int launch_wgrad4s2(const bf16* dy, const bf16* x, float* ws, int B, int 
   if (tiles >= (1L << 31)) { s3od_set_error("wgrad 4s2: too many tiles"); return 22; }
     const int nci = CinT / 64, nblk = (CoT / 64) * nci;
   const int wpc = (int)std::max<long>(1, std::min<long>(tiles, std::max(1, s3od_cu_count() / nblk)));
-  hipLaunchKernelGGL(kfn, dim3(nblk * wpc), dim3(256), wg4::LDS, st, dy, x, ws, OH, OW, tx, ty, (int)tiles, CinT, CoT, nci, wpc);
+  hipLaunchKernelGGL(kfn, dim3(nblk * wpc), dim3(256), wg4::LDS, st, dy, x, ws, OH, OW, tx, ty, (int)tiles, CinT, CoT, nci, wpc,
+                     S3OD_KNOB("S3OD_WGD_YMAJ", 1));
   return s3od_check_launch("conv4s2_wgrad_dma");
 }
 
@@ -1561,10 +1565,22 @@ static int conv_wgrad_pp_split(int dtype, int B, int H, int W, int Cin, int OH, 
 }
 
 // bytes of the slab workspace s3od_conv_wgrad uses for these arguments (0 = none needed)
+// The LDS-DMA 3x3 weight gradient (wgrad_dma.hip) takes every 3x3 s1 p1 bf16 conv whose tiles are whole (H % 8,
+// W % 32), input channels a multiple of 64 and output channels a multiple of 64 (or the 96 of the mask heads, Cin 64).
+// Measured at bs 16 against the ping-pong Wgrad3B kernel (tools/wgrad_bench.py big, same box): 256^2 256->256
+// 1523-1571 vs 822-834 us, 128^2 256->256 401 vs 215, 128^2 512->256 755 vs 394, 64^2 1024->256 425 vs 220,
+// 64^2 256->256 128 vs 84.  S3OD_WGRAD_DMA=0 restores the earlier routing.
+static bool wgrad_dma_ok(int dtype, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW, int stride, int pad) {
+  return dtype == S3OD_BF16 && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W && Cin % 64 == 0 &&
+         (Cout % 64 == 0 || (Cout == 96 && Cin == 64)) && H % HT_TH == 0 && W % HT_TW == 0 &&
+         (long)H * W * (Cin > Cout ? Cin : Cout) * 2 < (1L << 31) && !S3OD_OFF("S3OD_WGRAD_DMA");
+}
+
 int s3od_conv_wgrad_ws(int dtype, int B, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW, int stride,
                        int pad, int split, long* bytes) {
   S3OD_REQUIRE(bytes != nullptr, "conv_wgrad_ws: null output");
-  const int sp = slab_ok() ? conv_wgrad_pp_split(dtype, B, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad, split) : 0;
+  const int sp = slab_ok() && !wgrad_dma_ok(dtype, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad)
+                     ? conv_wgrad_pp_split(dtype, B, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad, split) : 0;
   *bytes = sp > 1 ? 4L * sp * Cout * KH * KW * Cin : 0;
   return 0;
 }
@@ -1595,13 +1611,12 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
     return s3od_check_launch("conv_wgrad permute");
   }
   const int coblk = Cout % 64 == 0 ? 64 : (Cout == 96 ? 96 : 0);
-  if (wg_knob && dtype == S3OD_BF16 && ws && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W &&
-      Cin % 64 == 0 && coblk && (Cin == 64 || (long)H * W >= 512L * 512)) {
-    // the LDS-DMA kernel works on 64 x 64 channel blocks; the 96-output-channel mask heads (Cin 64) run as two output
-    // blocks, the second reading 32 channels past each pixel's 96 (finite data of the next pixel, zeros past the image)
-    // whose products are never flushed
-    const bool dma = (coblk == 64 || (coblk == 96 && Cin == 64)) && (long)H * W * (Cin > Cout ? Cin : Cout) * 2 < (1L << 31) &&
-                     H % HT_TH == 0 && W % HT_TW == 0 && !S3OD_OFF("S3OD_WGRAD_DMA");
+  // the LDS-DMA kernel works on 64 x 64 channel blocks; the 96-output-channel mask heads (Cin 64) run as two output
+  // blocks, the second reading 32 channels past each pixel's 96 (finite data of the next pixel, zeros past the image)
+  // whose products are never flushed
+  const bool dma = wg_knob && ws && wgrad_dma_ok(dtype, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad);
+  if (dma || (wg_knob && dtype == S3OD_BF16 && ws && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W &&
+              Cin % 64 == 0 && coblk && (Cin == 64 || (long)H * W >= 512L * 512))) {
     int rc = dma ? wgrad3x3_dma_launch(relu_x, (const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st) :
              coblk == 64 ? (relu_x ? launch_wgrad_halo<64, true>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st)
                                    : launch_wgrad_halo<64, false>((const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st))

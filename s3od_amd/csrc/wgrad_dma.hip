@@ -163,7 +163,7 @@ conv3x3_wgrad_dma_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x
 template <bool RELU, int NPROD>
 __global__ void __launch_bounds__(64 * (4 + NPROD), 1)
 conv3x3_wgrad_dmap_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x, float* __restrict__ ws, int H, int W,
-                          int tiles_x, int tiles_y, int ntiles, int CinT, int CoT, int nci, int wpc) {
+                          int tiles_x, int tiles_y, int ntiles, int CinT, int CoT, int nci, int wpc, int ymaj) {
   using namespace wgd;
   constexpr int NCO = 4, NP = 9, DP = DYB / 1024, HP = PIECES - DP;    // 32 dy + 44 halo pieces
   constexpr int DPP = DP / NPROD, HPP = HP / NPROD;                    // per producer
@@ -189,7 +189,11 @@ conv3x3_wgrad_dmap_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ 
       hcode[j / 8] |= code << (4 * (j % 8));
     }
     auto issue = [&](int tile, int slot) __attribute__((always_inline)) {
-      const int txi = tile % tiles_x, t2 = tile / tiles_x, tyi = t2 % tiles_y, b = t2 / tiles_y;
+      // ymaj: a workgroup's consecutive tiles walk DOWN a column of tiles, so each halo shares its top 2 rows with the
+      // previous tile's (read moments ago: L2) -- 8 of 10 halo rows per tile from HBM instead of 10
+      int txi, tyi, b;
+      if (ymaj) { tyi = tile % tiles_y; const int t2 = tile / tiles_y; txi = t2 % tiles_x; b = t2 / tiles_x; }
+      else { txi = tile % tiles_x; const int t2 = tile / tiles_x; tyi = t2 % tiles_y; b = t2 / tiles_y; }
       const int ty0 = tyi * HT_TH, tx0 = txi * HT_TW;
       const long img_d = (long)H * W * CoT, img_x = (long)H * W * CinT;
       const long od = ((long)ty0 * W + tx0) * CoT + co0, ox = ((long)(ty0 - 1) * W + tx0 - 1) * CinT + ci0;
@@ -306,7 +310,7 @@ static int launch_wgrad_dma(const bf16* dy, const bf16* x, float* ws, int B, int
   const int wpc = (int)std::max<long>(1, std::min<long>(tiles, std::max(1, s3od_cu_count() / nblk)));
   if (prod)
     hipLaunchKernelGGL(kp, dim3(nblk * wpc), dim3(64 * (4 + (np == 4 || np == 2 ? np : 1))), wgd::LDS, st, dy, x, ws, H, W, tx, ty, (int)tiles,
-                       CinT, CoT, nci, wpc);
+                       CinT, CoT, nci, wpc, S3OD_KNOB("S3OD_WGD_YMAJ", 1));
   else
     hipLaunchKernelGGL(conv3x3_wgrad_dma_kernel<RELU>, dim3(nblk * wpc), dim3(256), wgd::LDS, st, dy, x, ws, H, W, tx, ty, (int)tiles, CinT, CoT, nci, wpc);
   return s3od_check_launch("conv3x3_wgrad_dma");

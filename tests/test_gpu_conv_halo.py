@@ -109,10 +109,13 @@ def test_conv_wgrad_halo(cout, B, H, W, relu):
 
 
 @pytest.mark.parametrize("cin,cout,B,H,W,relu", [(256, 256, 2, 20, 36, True), (128, 192, 1, 512, 520, True),
-                                                  (256, 128, 1, 520, 512, False), (128, 128, 2, 512, 512, True)])
+                                                  (256, 128, 1, 520, 512, False), (128, 128, 2, 512, 512, True),
+                                                  (256, 256, 4, 64, 64, True), (512, 256, 2, 32, 64, False),
+                                                  (1024, 256, 1, 16, 32, False)])
 def test_conv_wgrad_halo_channel_blocks(cin, cout, B, H, W, relu):
-    """The halo wgrad over 64-channel blocks of wider convs (used from 512^2 maps: the output_conv1 shape;
-    smaller maps take the implicit GEMM, checked by the first case)."""
+    """The halo wgrad over 64-channel blocks of wider convs: the LDS-DMA kernel for every whole-tile shape (the RCU /
+    layerK_rn / output_conv1 weight gradients, down to one-tile-per-image maps), the register-staged one from 512^2
+    maps otherwise; the ragged small map takes the ping-pong / implicit GEMM (first case)."""
     from s3od_amd._lib import lib, stream
     g = torch.Generator(device="cuda").manual_seed(cin + cout)
     dy = torch.randn(B, cout, H, W, device="cuda", generator=g).bfloat16()

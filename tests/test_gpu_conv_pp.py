@@ -101,7 +101,8 @@ def test_conv_wgrad_pp(B, H, W, Ci, relu):
     """3x3 s1 weight gradient of a 256-output-channel conv on the ping-pong kernel (Wgrad3B loader: one tap's 256 input
     channels per tile, pixels split over the grid, fp32 atomics into the GEMM-layout workspace, then the permute),
     accumulated onto an existing gradient, vs torch's conv2d_weight of the same bf16 operands (ReLU'd input when
-    relu = 1: an RCU conv1); and vs the 128x128 implicit GEMM (S3OD_WGRAD_PP=0).  Odd H, several images per split."""
+    relu = 1: an RCU conv1); and vs the 128x128 implicit GEMM (S3OD_WGRAD_PP=0).  Odd H, several images per split.
+    Whole-tile shapes (H % 8, W % 32) take the LDS-DMA kernel by default; S3OD_WGRAD_DMA=0 keeps them here."""
     from s3od_amd._lib import lib, stream
     Co = 256
     g = torch.Generator(device="cuda").manual_seed(B * H + Ci)
@@ -113,18 +114,22 @@ def test_conv_wgrad_pp(B, H, W, Ci, relu):
     ws = torch.zeros(Co * 9 * Ci, device="cuda")
     import ctypes
     nb = ctypes.c_long(0)
+    os.environ["S3OD_WGRAD_DMA"] = "0"
     lib()("s3od_conv_wgrad_ws", BF16, B, H, W, Ci, H, W, Co, 3, 3, 1, 1, 0, ctypes.addressof(nb))
+    os.environ.pop("S3OD_WGRAD_DMA", None)
     # the caller-owned split-K slab (poisoned: every word read back must have been written)
     slab = torch.full((max(nb.value, 4) // 4,), float("nan"), device="cuda") if nb.value else None
     outs = {}
     for knob, sl in (("1", None), ("1", slab), ("0", None)):
         dw = dw0.clone()
         os.environ["S3OD_WGRAD_PP"] = knob
+        os.environ["S3OD_WGRAD_DMA"] = "0"
         try:
             lib()("s3od_conv_wgrad", BF16, B, H, W, Ci, H, W, Co, 3, 3, 1, 1, _nhwc(dy), _nhwc(x), relu, dw, ws, 0, sl,
                   nb.value if sl is not None else 0, stream())
         finally:
             os.environ.pop("S3OD_WGRAD_PP", None)
+            os.environ.pop("S3OD_WGRAD_DMA", None)
         torch.cuda.synchronize()
         err = float((dw - ref).norm() / (ref - dw0).norm())
         assert err < 1e-5, (knob, sl is not None, err)

@@ -57,6 +57,32 @@ def main():
             print(f"  wave {w}: {nm[0]} {float((e[:, 0] / n[:, 0]).mean()):.3f} {nm[1]} {float((e[:, 1] / n[:, 0]).mean()):.3f}"
                   f" {nm[2]} {float((e[:, 2] / n[:, 0]).mean()):.3f}  span {float((e[:, 4] - e[:, 3]).mean()):.1f} us")
         return
+    if sys.argv[1:2] == ["big"]:                  # the 256-channel RCU / layerK_rn weight gradients: ping-pong (DMA=0) vs LDS-DMA
+        for (H, cin, cout, relu) in ((256, 256, 256, 0), (256, 256, 256, 1), (128, 256, 256, 0), (128, 512, 256, 0),
+                                     (64, 256, 256, 0), (64, 1024, 256, 0)):
+            dy = torch.randn(B, H, H, cout, device="cuda").bfloat16()
+            x = torch.randn(B, H, H, cin, device="cuda").bfloat16()
+            ws = torch.zeros(cout * 9 * cin, device="cuda")
+            import ctypes
+            nb = ctypes.c_long(0)
+            os.environ["S3OD_WGRAD_DMA"] = "0"             # the ping-pong arm's slab size
+            lib()("s3od_conv_wgrad_ws", BF16, B, H, H, cin, H, H, cout, 3, 3, 1, 1, 0, ctypes.addressof(nb))
+            slab = torch.zeros(max(nb.value, 4) // 4, device="cuda")
+            fl = 2.0 * B * H * H * cin * cout * 9
+            res = {}
+            for rnd in range(3):
+                for knob in ("0", "1"):
+                    os.environ["S3OD_WGRAD_DMA"] = knob
+                    dw = torch.zeros(cout, cin, 3, 3, device="cuda")
+                    f = lambda: lib()("s3od_conv_wgrad", BF16, B, H, H, cin, H, H, cout, 3, 3, 1, 1, dy, x, relu, dw, ws, 0, slab,
+                                      nb.value, stream())
+                    t = timeit(f)
+                    dw.zero_(); f(); torch.cuda.synchronize(); res[knob] = dw.clone()
+                    print(f"{H}^2 {cin}->{cout} relu {relu} round {rnd} DMA={knob}: {t * 1e6:8.1f} us {fl / t / 1e12:7.1f} TF/s", flush=True)
+            a, b = res["1"], res["0"]
+            print(f"   max |dma - pp| / max|pp| = {float((a - b).abs().max() / b.abs().max()):.3e}")
+        os.environ.pop("S3OD_WGRAD_DMA", None)
+        return
     if sys.argv[1:2] == ["xp"]:                   # experiment: A/B of a dev knob (argv[2], values argv[3:]) at 1024^2 64 -> 64
         H, cin, cout = 1024, 64, 64                # (XP_SHAPE=512: 512^2 256 -> 128 with the ReLU'd input)
         relu = 0
