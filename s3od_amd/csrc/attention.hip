@@ -128,6 +128,7 @@ __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(const T* __restrict__ 
   const T* Kp = K + (long)bh * N * 64;
   const T* Vp = V + (long)bh * N * 64;
   const int q0 = blockIdx.x * 128 + wave * 32;
+  const bool active = q0 < N;        // wave-uniform
 
   // Q fragments (B operand of S^T = K Q^T): lane holds Q[q0 + qs*16 + li][d-slice of group g]
   constexpr int QK = F32 ? 16 : 2;     // k-steps over d=64
@@ -181,6 +182,8 @@ __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(const T* __restrict__ 
     if (more) stage_load((kt + 1) * 64);
     const char* ks = smem + cur * 2 * L::BYTES;
     const char* vs = ks + L::BYTES;
+    // a wave whose 32 queries are all >= N (the partial last block: N = 4096 + 5 prefix tokens) only helps stage K / V
+    if (active) {
     // ---- S^T = K Q^T (- m) : acc[kb][qs], element i: key = kb*16 + 4g + i, query = qs*16 + li
     f32x4 s[4][2];
 #pragma unroll
@@ -295,6 +298,7 @@ __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(const T* __restrict__ 
         lacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[0], lacc[0], 0, 0, 0);
         lacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[1], lacc[1], 0, 0, 0);
       }
+    }
     }
     if (more) stg.store(smem + (cur ^ 1) * 2 * L::BYTES, smem + (cur ^ 1) * 2 * L::BYTES + L::BYTES, tid);
     __syncthreads();
@@ -980,6 +984,7 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __r
   ddo.init(ldo * 2, wave, lane);
   const unsigned vrow = lane < 16 ? 16u * lane : 0x80000000u;
   const int k0 = blockIdx.x * (32 * W) + wave * 32;
+  const bool active = k0 < N;        // wave-uniform
   bf16x8 kf[4], vf[4];
   {
     const int key = k0 + (lane & 31);
@@ -1048,15 +1053,17 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __r
         for (int db = 0; db < 2; db++) { dv[db] = mma32(pa[qb][st], bo[db], dv[db]); dk[db] = mma32(da[qb][st], bq[db], dk[db]); }
       }
     };
-    sdp(0);
-    __builtin_amdgcn_sched_barrier(0);
-    sdp(1);
-    softmax(0);
-    __builtin_amdgcn_sched_barrier(0);
-    dvdk(0);
-    softmax(1);
-    __builtin_amdgcn_sched_barrier(0);
-    dvdk(1);
+    if (active) {      // a wave past the partial last block only stages tiles
+      sdp(0);
+      __builtin_amdgcn_sched_barrier(0);
+      sdp(1);
+      softmax(0);
+      __builtin_amdgcn_sched_barrier(0);
+      dvdk(0);
+      softmax(1);
+      __builtin_amdgcn_sched_barrier(0);
+      dvdk(1);
+    }
     __syncthreads();      // drains this tile's reads and the next tile's LDS-DMA (vmcnt(0)) before the flip
   };
   int qt = 0;
@@ -1097,6 +1104,7 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __res
   Dma64R<W> dkv;
   dkv.init(128, wave, lane);
   const int q0 = blockIdx.x * (32 * W) + wave * 32;
+  const bool active = q0 < N;        // wave-uniform
   bf16x8 qf[4], of[4];
   f32x16 cl, cd;     // C operands: LSE (log2 units) / delta of the lane's query, all 16 rows
   {
@@ -1161,15 +1169,17 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __res
         for (int db = 0; db < 2; db++) dq[db] = mma32(da[kb][st], bk[db], dq[db]);
       }
     };
-    sdp(0);
-    __builtin_amdgcn_sched_barrier(0);
-    sdp(1);
-    softmax(0);
-    __builtin_amdgcn_sched_barrier(0);
-    dqk(0);
-    softmax(1);
-    __builtin_amdgcn_sched_barrier(0);
-    dqk(1);
+    if (active) {      // a wave past the partial last block only stages tiles
+      sdp(0);
+      __builtin_amdgcn_sched_barrier(0);
+      sdp(1);
+      softmax(0);
+      __builtin_amdgcn_sched_barrier(0);
+      dqk(0);
+      softmax(1);
+      __builtin_amdgcn_sched_barrier(0);
+      dqk(1);
+    }
     __syncthreads();
   };
   int kt = 0;
