@@ -1442,8 +1442,11 @@ static int conv_fwd_igemm(int dtype, ConvGeo g, int M, int N, int K, int Cin, in
         return relu_in ? pp(std::true_type{}) : pp(std::false_type{});
       }
     }
+    // 128-output-channel 3x3 convs over >= 2M pixels (output_conv1 at 512^2): 256x128 tiles, 3 stages (one workgroup
+    // per CU) -- 2630 vs 2765 us at bs 16 (tools/lin_sweep.py, S3OD_GEMM_CFG 0 vs 1); S3OD_CONV_N128_CFG picks another
+    const int def = Cout <= 64 ? 3 : (g.KH == 3 && Cout < 256 && M >= (1 << 21)) ? S3OD_KNOB("S3OD_CONV_N128_CFG", 0) : 1;
     auto go = [&](auto bn, auto rl) -> int {
-      return with_cfg<T>(Cout <= 64 ? 3 : 1, [&](auto C0) -> int {
+      return with_cfg<T>(def, [&](auto C0) -> int {
         typedef ConvCfg<decltype(C0), decltype(bn)::value> CC;
         constexpr int BM = CC::BM, NST = CC::NST;
         constexpr int BN = decltype(bn)::value < CC::BN ? decltype(bn)::value : CC::BN;
