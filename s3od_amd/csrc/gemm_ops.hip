@@ -1414,6 +1414,9 @@ static bool conv_pp_ok(const ConvGeo& g, int M, int N, bool stats) {
   const long tiles = (long)(M / 256) * (N / 256);
   const int min_ns = S3OD_KNOB("S3OD_CONV_PP_MIN", 512) > 0 ? S3OD_KNOB("S3OD_CONV_PP_MIN", 512) : 512;
   const bool rounds = tiles >= 2048 || g.SC >= 512 || (tiles >= min_ns && (!stats || S3OD_KNOB("S3OD_CONV_PP", -1) == 2));
+  // 128-channel inputs (the output_conv1 data gradient, K = 9 x 128): the ping-pong kernel's per-tap A tiles are half
+  // width there and the generic path measured faster in the whole step (150.1 -> 147.5 ms median, same box)
+  if (g.SC < 256 && !S3OD_KNOB("S3OD_CONV_PP_SC128", 0)) return false;
   return tl_cfg < 0 && gemm_cfg() < 0 && g.KH == 3 && g.KW == 3 && g.s == 1 && g.p == 1 && g.RH == g.SH && g.RW == g.SW &&
          g.SC % 64 == 0 && (nch & (nch - 1)) == 0 && N % 256 == 0 && pp_pays(M, N) && rounds && !S3OD_OFF("S3OD_CONV_PP");
 }
