@@ -202,9 +202,15 @@ template <int CI> struct RwShape {
 // Every wave issues a FIXED sequence of vector-memory instructions per tile (PPW DMA pieces, PB mask loads, PB stores:
 // dummy pieces / out-of-image lanes use an out-of-range buffer offset instead of a branch), so the counted vmcnt
 // that retires a tile's halo is a per-phase constant.
+// GB > 0 (MODE 0-2): the tile's PB blocks run in groups of GB (all 9 * KK steps of one group's GB x NB accumulators,
+// then the next group's), and each group's epilogue (ReLU / mask, lane-pair trade, pack, store) is issued between the
+// NEXT group's MFMAs -- the last group's carried into the next tile's first group (a dummy group with out-of-range
+// stores before the first tile) -- so with one wave per SIMD the matrix pipe no longer idles through the epilogue.
+// Same MFMA chain per accumulator (outputs bit-identical to GB = 0); per tile still PB stores after the halo issue,
+// so the counted waits are unchanged.
 typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
-template <int MODE, int CI>
+template <int MODE, int CI, int GB>
 __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                                  const float* __restrict__ bias,
                                                                  const bf16* __restrict__ res1, float* __restrict__ colsum,
@@ -215,6 +221,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
   constexpr int PB = S::PB, PPW = S::PPW, NPC = S::NPC, HC = S::HC, ROWB = S::ROWB;
   constexpr int NB = MODE == 3 ? 3 : 2, CO = 32 * NB;     // 16-channel blocks per wave / output channels
   static_assert(MODE != 3 || (CI == 64 && NPC == 2), "mask heads: 64 input channels, 8 x 32 tiles");
+  static_assert(GB == 0 || (MODE != 3 && PB % GB == 0), "grouped epilogue: modes 0-2, whole groups");
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int lr = lane & 15, lg = lane >> 4, odd = lg & 1;
@@ -280,6 +287,48 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
   __syncthreads();
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
+  // GB > 0: the carried group (accumulators, store offsets, masks, output descriptor); a dummy before the first tile
+  constexpr int GBC = GB > 0 ? GB : 1;
+  f32x4 cacc[GBC][NB];
+  unsigned cpo[GBC];
+  u32x4v crm[GBC];
+#pragma unroll
+  for (int q = 0; q < GBC; q++) {
+    cpo[q] = 0x80000000u;
+    crm[q] = u32x4v{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int nb = 0; nb < NB; nb++) cacc[q][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  int cbb = 0;                                        // batch index of the carried group's tile
+  // epilogue of one 16-px block: lane holds out[px = block, lr][co = ch0 + 16 nb + 4 lg .. +3]; v_permlane16_swap
+  // trades rows 1 / 3 of the first operand with rows 0 / 2 of the second (row = 16 lanes = one lg): the even lg keeps
+  // its nb 0 and receives the odd partner's nb 0, the odd lg keeps nb 1 and receives the even's -> channels cb .. cb+7
+  // (the output descriptor is built here from the batch index: a descriptor carried across tiles in SGPRs lost its
+  // range word under hipcc 7.2 -- the mode-1 instance's in-tile group stores were dropped)
+  auto epi_blk = [&](const f32x4 (&a)[NB], unsigned p, u32x4v mraw, int bbx) {
+    const auto r = make_rsrc(out + bbx * img_o, out ? (unsigned long)img_o * 2 : 0ul);
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      float v0 = a[0][e], v1 = a[1][e];
+      if (MODE == 2) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); }
+      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(v0), __float_as_uint(v1), false, false);
+      o[e] = __uint_as_float(sw[0]);               // channels cb + 0..3
+      o[4 + e] = __uint_as_float(sw[1]);           // channels cb + 4..7
+    }
+    if constexpr (MODE == 1) {
+      const bf16x8 m = __builtin_bit_cast(bf16x8, mraw);
+#pragma unroll
+      for (int e = 0; e < 8; e++) o[e] = (float)m[e] > 0.f ? o[e] : 0.f;   // out-of-image lanes: mask reads 0
+#pragma unroll
+      for (int e = 0; e < 8; e++) cs[e] += o[e];     // column sums of channels cb .. cb+7 (lane partials)
+    }
+    bf16x8 ob;
+#pragma unroll
+    for (int e = 0; e < 8; e++) ob[e] = (bf16)o[e];
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, ob), r, p, 0, 0);
+  };
+
   int tile = t_beg + wi, k = 0;
   issue(tile, 0);
   issue(tile + wpx, 1);
@@ -310,6 +359,59 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
     asm volatile("" ::: "memory");
     issue(tile + 2 * wpx, (k + 2) % 3);
     const char* hb = smem + (k % 3) * S::BUF;
+    constexpr int NST = 9 * S::KK;
+    if constexpr (GB > 0) {
+      // fragments of group gi's GB blocks for step st; the group's MFMAs; the carried group's epilogue in the first
+      // GB step pairs
+      auto rd_g = [&](int gi, int st, bf16x8 (&fa)[GB]) {
+        const int tap = st / S::KK, kk = st % S::KK, dy = tap / 3, dx = tap - 3 * (tap / 3);
+#pragma unroll
+        for (int q = 0; q < GB; q++) {
+          const int pb = gi * GB + q, off = (pb / NPC + dy) * HC + (pb % NPC) * 16 + dx;
+          fa[q] = *(const bf16x8*)(hb + yb[off & 7][kk] + off * ROWB);
+        }
+      };
+#pragma unroll
+      for (int gi = 0; gi < PB / GB; gi++) {
+        f32x4 acc[GB][NB];
+#pragma unroll
+        for (int nb = 0; nb < NB; nb++) {
+          const f32x4 b0 = MODE != 1 ? *(const f32x4*)(aux + ch0 + nb * 16 + 4 * lg) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int q = 0; q < GB; q++) acc[q][nb] = b0;
+        }
+        auto mm_g = [&](int st, const bf16x8 (&fa)[GB]) {
+#pragma unroll
+          for (int q = 0; q < GB; q++)
+#pragma unroll
+            for (int nb = 0; nb < NB; nb++)
+              acc[q][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[st / S::KK][st % S::KK][nb], fa[q], acc[q][nb], 0, 0, 0);
+        };
+        bf16x8 fa0[GB], fa1[GB];
+        rd_g(gi, 0, fa0);
+#pragma unroll
+        for (int st = 0; st < NST; st += 2) {
+          if (st + 1 < NST) rd_g(gi, st + 1, fa1);
+          __builtin_amdgcn_sched_barrier(0);
+          mm_g(st, fa0);
+          if (st / 2 < GB) epi_blk(cacc[st / 2], cpo[st / 2], crm[st / 2], cbb);
+          __builtin_amdgcn_sched_barrier(0);
+          if (st + 2 < NST) rd_g(gi, st + 2, fa0);
+          __builtin_amdgcn_sched_barrier(0);
+          if (st + 1 < NST) mm_g(st + 1, fa1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int q = 0; q < GB; q++) {
+#pragma unroll
+          for (int nb = 0; nb < NB; nb++) cacc[q][nb] = acc[q][nb];
+          cpo[q] = po[gi * GB + q];
+          if constexpr (MODE == 1) crm[q] = rm_[gi * GB + q];
+        }
+        cbb = bb;
+      }
+      continue;
+    }
     f32x4 acc[PB][NB];                                // acc[pb][nb]: D[co = ch0 + 16 nb + 4 lg + e][px = block pb, lr]
 #pragma unroll
     for (int nb = 0; nb < NB; nb++) {
@@ -318,7 +420,6 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
       for (int pb = 0; pb < PB; pb++) acc[pb][nb] = b0;
     }
     // 9 * KK (tap, k-chunk) steps of 2 PB MFMAs; the next step's PB halo fragments are read before this step's MFMAs
-    constexpr int NST = 9 * S::KK;
     auto rd = [&](int st, bf16x8 (&fa)[PB]) {
       const int tap = st / S::KK, kk = st % S::KK, dy = tap / 3, dx = tap - 3 * (tap / 3);
 #pragma unroll
@@ -412,33 +513,13 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
         (void)pb;
       }
     } else {
-    // epilogue: lane holds out[px = block pb, lr][co = ch0 + 16 nb + 4 lg .. +3]; v_permlane16_swap trades rows 1 / 3
-    // of the first operand with rows 0 / 2 of the second (row = 16 lanes = one lg): the even lg keeps its nb 0 and
-    // receives the odd partner's nb 0, the odd lg keeps nb 1 and receives the even's -> 8 channels cb .. cb+7
 #pragma unroll
-    for (int pb = 0; pb < PB; pb++) {
-      float o[8];
-#pragma unroll
-      for (int e = 0; e < 4; e++) {
-        float v0 = acc[pb][0][e], v1 = acc[pb][1][e];
-        if (MODE == 2) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); }
-        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(v0), __float_as_uint(v1), false, false);
-        o[e] = __uint_as_float(sw[0]);               // channels cb + 0..3
-        o[4 + e] = __uint_as_float(sw[1]);           // channels cb + 4..7
-      }
-      if constexpr (MODE == 1) {
-        const bf16x8 m = __builtin_bit_cast(bf16x8, rm_[pb]);
-#pragma unroll
-        for (int e = 0; e < 8; e++) o[e] = (float)m[e] > 0.f ? o[e] : 0.f;   // out-of-image lanes: mask reads 0
-#pragma unroll
-        for (int e = 0; e < 8; e++) cs[e] += o[e];     // column sums of channels cb .. cb+7 (lane partials)
-      }
-      bf16x8 ob;
-#pragma unroll
-      for (int e = 0; e < 8; e++) ob[e] = (bf16)o[e];
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, ob), ro, po[pb], 0, 0);
+      for (int pb = 0; pb < PB; pb++) epi_blk(acc[pb], po[pb], rm_[pb], bb);
     }
-    }
+  }
+  if constexpr (GB > 0) {                             // the last tile's carried group
+#pragma unroll
+    for (int q = 0; q < GB; q++) epi_blk(cacc[q], cpo[q], crm[q], cbb);
   }
   if (MODE == 1 && colsum) {                          // 16 lanes (lr) -> 1, LDS atomics, one global add per channel
 #pragma unroll
@@ -457,12 +538,11 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
 static bool rw_ok(int dtype, int B, int H, int W) {
   return dtype == S3OD_BF16 && !S3OD_OFF("S3OD_CONV_RW") && (long)H * W * 192 < (1L << 31) && B > 0;
 }
-template <int MODE, int CI>
-static int launch_rw(const bf16* x, const bf16* w, const float* bias, const bf16* res1, float* colsum, bf16* out,
-                     int B, int H, int W, hipStream_t st, const float* w2 = nullptr, const float* b2 = nullptr,
-                     float* logits = nullptr) {
+template <int MODE, int CI, int GB>
+static int launch_rw_g(const bf16* x, const bf16* w, const float* bias, const bf16* res1, float* colsum, bf16* out,
+                       int B, int H, int W, hipStream_t st, const float* w2, const float* b2, float* logits) {
   typedef RwShape<CI> S;
-  auto kfn = conv3x3_c64_rw_kernel<MODE, CI>;
+  auto kfn = conv3x3_c64_rw_kernel<MODE, CI, GB>;
   static const bool attr = ((void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS), true);   // once per process (thread-safe static init)
   (void)attr;
   const int tx = cdiv(W, S::TW), ty = cdiv(H, S::TH);
@@ -472,6 +552,22 @@ static int launch_rw(const bf16* x, const bf16* w, const float* bias, const bf16
   hipLaunchKernelGGL(kfn, dim3(nwg), dim3(256), S::LDS, st, x, w, bias, res1, colsum, out, H, W, tx, ty, (int)tiles, w2, b2,
                      logits);
   return s3od_check_launch("conv3x3_c64_rw");
+}
+// modes 0-2: the grouped epilogue (S3OD_RW_GB = blocks per group: 2 default, 4, or 0 = the epilogue after all MFMAs).
+// Measured (tools/conv64_bench.py, bs 16 x 1024^2 64 -> 64 + ReLU, same box): GB 0 1290-1309 us, GB 2 1225-1242,
+// GB 4 1251-1280 (profiles/r05t_rw_grouped_epilogue.txt)
+template <int MODE, int CI>
+static int launch_rw(const bf16* x, const bf16* w, const float* bias, const bf16* res1, float* colsum, bf16* out,
+                     int B, int H, int W, hipStream_t st, const float* w2 = nullptr, const float* b2 = nullptr,
+                     float* logits = nullptr) {
+  if constexpr (MODE != 3) {
+    // the masked data gradient (mode 1) stays on GB = 0 unless S3OD_RW_GB1=1: its grouped instance miscompiles under
+    // hipcc 7.2 (in-tile group stores dropped / masks misapplied; tools/rw_gb_diff.py)
+    const int gb = MODE == 1 && !S3OD_KNOB("S3OD_RW_GB1", 0) ? 0 : S3OD_KNOB("S3OD_RW_GB", 2);
+    if (gb == 4) return launch_rw_g<MODE, CI, 4>(x, w, bias, res1, colsum, out, B, H, W, st, w2, b2, logits);
+    if (gb == 2) return launch_rw_g<MODE, CI, 2>(x, w, bias, res1, colsum, out, B, H, W, st, w2, b2, logits);
+  }
+  return launch_rw_g<MODE, CI, 0>(x, w, bias, res1, colsum, out, B, H, W, st, w2, b2, logits);
 }
 
 // ---------------------------------------------------------------- register-weight ConvTranspose2d(128, 64, 4, s2, p1)

@@ -65,6 +65,52 @@ def test_conv_dgrad_relu_mask_and_colsum(cout_fwd):
     assert float((cs - ref_cs).abs().max()) <= float(tol), (float((cs - ref_cs).abs().max()), float(tol))
 
 
+@pytest.mark.parametrize("gb", ["2", "4"])
+def test_rw_grouped_epilogue_bit_identical(gb):
+    """The grouped epilogue (S3OD_RW_GB: each group's epilogue issued between the next group's MFMAs, the last group's
+    carried into the next tile) runs the same MFMA chain per accumulator: outputs bit-identical to S3OD_RW_GB=0 for
+    the forward (bias + ReLU).  The masked 64 / 96-channel data gradients stay on GB = 0 (their grouped instance
+    miscompiles, S3OD_RW_GB1): checked unchanged under the knob; column sums to fp32 summation order."""
+    from s3od_amd._lib import lib, stream
+    B, H, W = 3, 37, 70                                    # ragged: partial tiles, several tiles per workgroup
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randn(B, H, W, 64, device="cuda", generator=g).bfloat16()
+    wp = (torch.randn(64, 3, 3, 64, device="cuda", generator=g) * 0.06).bfloat16()
+    bias = torch.randn(64, device="cuda", generator=g) * 0.1
+    res1 = torch.randn(B, H, W, 64, device="cuda", generator=g).bfloat16()
+    dy96 = torch.randn(B, H, W, 96, device="cuda", generator=g).bfloat16()
+    w96 = (torch.randn(96, 3, 3, 64, device="cuda", generator=g) * 0.06).bfloat16()
+    w96T = w96.flip(1, 2).permute(3, 1, 2, 0).contiguous()
+    wT = wp.flip(1, 2).permute(3, 1, 2, 0).contiguous()
+
+    def run():
+        of = torch.empty(B, H, W, 64, device="cuda", dtype=torch.bfloat16)
+        lib()("s3od_conv_fwd", BF16, B, H, W, 64, H, W, 64, 3, 3, 1, 1, x, 0, wp, bias, None, None, ACT_RELU, None, None,
+              of, None, None, None, stream())
+        outs = [of]
+        for co, d, ww, wt in ((64, x, wp, wT), (96, dy96, w96, w96T)):
+            dx = torch.empty(B, H, W, 64, device="cuda", dtype=torch.bfloat16)
+            cs = torch.zeros(64, device="cuda")
+            lib()("s3od_conv_dgrad", BF16, B, H, W, 64, H, W, co, 3, 3, 1, 1, d, ww, None, None, None, ACT_RELU_BWD, res1,
+                  None, dx, None, None, cs, wt, stream())
+            outs += [dx, cs]
+        torch.cuda.synchronize()
+        return outs
+
+    try:
+        os.environ["S3OD_RW_GB"] = "0"
+        ref = run()
+        os.environ["S3OD_RW_GB"] = gb
+        got = run()
+    finally:
+        os.environ.pop("S3OD_RW_GB", None)
+    for i, (a, b) in enumerate(zip(got, ref)):
+        if a.dtype == torch.bfloat16:
+            assert torch.equal(a, b), i
+        else:
+            assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max()) + 1e-3, i
+
+
 def test_mask_heads_fwd_halo():
     from s3od_amd._lib import lib, stream
     B, H, W, NM = 2, 50, 41, 3

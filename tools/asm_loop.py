@@ -1,7 +1,7 @@
 """Instruction census of the largest loop of each kernel in a hipcc -S output (dev tool).
 
     hipcc --offload-arch=gfx950 -O3 ... --cuda-device-only -S x.hip -o x.s
-    python tools/asm_loop.py x.s [kernel-substring]
+    python tools/asm_loop.py x.s [kernel-substring] [salu]   (salu: scalar ops in the census too)
 """
 import re
 import sys
@@ -55,7 +55,7 @@ def main():
                 continue
             c = classify(t)
             cnt[c] = cnt.get(c, 0) + 1
-            if c == "valu":
+            if c == "valu" or (c == "salu" and len(sys.argv) > 3):
                 v[t] = v.get(t, 0) + 1
         vg = re.search(r"\.vgpr_count:\s+(\d+)", "\n".join(body))
         print(name[:90], "| loop lines", b - a)

@@ -2,7 +2,7 @@
 with the ReLU' mask and the bias column sums) at bs 16 x 1024^2: the register-weight kernel (default) vs the
 implicit GEMM (S3OD_CONV_RW=0, read per call), in one process, interleaved rounds; outputs compared (dev tool).
 
-    python tools/conv64_bench.py [B] [H]
+    python tools/conv64_bench.py [B] [H]        (ARMS=RW_GB=0,RW_GB=4: other S3OD_ knobs as the arms)
 """
 import os
 os.environ.setdefault("S3OD_AB", "1")   # knobs toggled per call (csrc/common.hpp S3OD_KNOB)
@@ -64,9 +64,13 @@ def main():
     def heads(lg, hs):
         lib()("s3od_mask_heads_fwd", BF16, B, H, W, 3, x, hw1, hb1, hw2, hb2, lg, hs, stream())
 
+    arms = os.environ.get("ARMS", "CONV_RW=0,CONV_RW=1").split(",")   # e.g. ARMS=RW_GB=0,RW_GB=2,RW_GB=4
     for rnd in range(3):
-        for rw in ("0", "1"):
-            os.environ["S3OD_CONV_RW"] = rw
+        for rw in arms:
+            kn, val = rw.split("=")
+            for a in arms:
+                os.environ.pop("S3OD_" + a.split("=")[0], None)
+            os.environ["S3OD_" + kn] = val
             of = torch.empty(B, H, W, 64, device="cuda", dtype=torch.bfloat16)
             od = torch.empty_like(of)
             cs = torch.zeros(64, device="cuda")
@@ -85,12 +89,12 @@ def main():
             outs[rw] = (of, od, cs.clone(), o96, cs96, lgt, hs)
             by_f = B * H * W * 64 * 2 * 2
             by_d = B * H * W * 64 * 2 * 3
-            print(f"round {rnd} RW={rw}: fwd {tf * 1e6:8.1f} us ({fl / tf / 1e12:6.1f} TF/s, {by_f / tf / 1e9:6.0f} GB/s) | "
+            print(f"round {rnd} {rw}: fwd {tf * 1e6:8.1f} us ({fl / tf / 1e12:6.1f} TF/s, {by_f / tf / 1e9:6.0f} GB/s) | "
                   f"dgrad {td * 1e6:8.1f} us ({fl / td / 1e12:6.1f} TF/s, {by_d / td / 1e9:6.0f} GB/s) | dgrad 64<-96 {t96 * 1e6:8.1f} us "
                   f"({fl * 1.5 / t96 / 1e12:6.1f} TF/s, {by_d * 3.5 / 3 / t96 / 1e9:6.0f} GB/s) | heads {th * 1e6:8.1f} us "
                   f"({fl * 1.5 / th / 1e12:6.1f} TF/s, {B * H * W * (128 + 192 + 12) / th / 1e9:6.0f} GB/s)", flush=True)
     for i, name in enumerate(("fwd", "dgrad", "colsum", "dgrad 64<-96", "colsum 64<-96", "head logits", "hsave")):
-        a, b = outs["0"][i].float(), outs["1"][i].float()
+        a, b = outs[arms[0]][i].float(), outs[arms[-1]][i].float()
         print(f"{name}: max |rw - igemm| / max|igemm| = {float((a - b).abs().max() / b.abs().max().clamp_min(1e-9)):.3e}")
 
 
