@@ -1413,12 +1413,22 @@ int s3od_linear_dgrad(int dtype, int M, int N, int K, const void* dy, long lddy,
   return 0;
 }
 
+// default tile config of a linear weight gradient: the 256x256 ping-pong kernel with split-K slabs for the large
+// outputs (3072x768 441 -> 403 us, 768x3072 457 -> 398, 2304x768 335 -> 308), 256x128 x 3 stages with fp32 atomics
+// otherwise.  S3OD_LWG_ROWS_PP=1 also puts the small outputs over >= 64K rows on the ping-pong kernel: faster alone
+// (tools/wgrad_sweep.py: 768x768 127 -> 110 us, 1024x768 154 -> 144, 256x256 x 1M rows 283 -> 268;
+// profiles/r05t_wgrad_sweep.txt) but null in the step, where these run on the side stream beside the data gradients
+// (tools/ab_step.py medians 151.4 vs 151.0 ms), so off by default
+static int linear_wgrad_def_cfg(int Nout, int Kin, int rows) {
+  const bool big_rows = rows >= 65536 && S3OD_KNOB("S3OD_LWG_ROWS_PP", 0);
+  return ((long)Nout * Kin > 1024L * 1024 || big_rows) ? 5 : 0;
+}
 // split-K slab floats a linear weight gradient uses (0: the fp32-atomic epilogue, no slab): the ping-pong kernel's
 // split-K partials go to sp caller-owned fp32 slabs [sp][Nout][Kin], summed by wgrad_reduce_kernel
 static long linear_wgrad_slab_floats(int dtype, int Nout, int Kin, int rows, int split) {
   if (dtype != S3OD_BF16 || !slab_ok() || Kin % 4 != 0) return 0;
   const int KTILES = cdiv(rows, KT<bf16>::BK);
-  const int def = (long)Nout * Kin <= 1024L * 1024 ? 0 : 5;
+  const int def = linear_wgrad_def_cfg(Nout, Kin, rows);
   return with_cfg<bf16>(def, [&](auto C) -> long {
     if constexpr (!decltype(C)::PP) return 0;
     else {
@@ -1445,9 +1455,7 @@ int s3od_linear_wgrad(int dtype, int Nout, int Kin, int rows, const void* dy, lo
   if (need == 0 || slab_bytes < 4 * need) slab = nullptr;
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(rows, KT<T>::BK);
-    // measured (tools/lin_sweep.py, bs16 1024^2 ViT shapes): the 256x256 ping-pong kernel for the large
-    // outputs (3072x768 441 -> 403 us, 768x3072 457 -> 398, 2304x768 335 -> 308), 256x128 for 768x768
-    const int def = (long)Nout * Kin <= 1024L * 1024 ? 0 : 5;
+    const int def = linear_wgrad_def_cfg(Nout, Kin, rows);
     return with_cfg<T>(def, [&](auto C) -> int {
       constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
       int sp = split > 0 ? split : wgrad_split<T, BM, BN, NST>(cdiv(Nout, BM) * cdiv(Kin, BN), KTILES);
