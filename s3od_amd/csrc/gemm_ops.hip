@@ -561,9 +561,11 @@ static int launch_rw(const bf16* x, const bf16* w, const float* bias, const bf16
                      int B, int H, int W, hipStream_t st, const float* w2 = nullptr, const float* b2 = nullptr,
                      float* logits = nullptr) {
   if constexpr (MODE != 3) {
-    // the masked data gradient (mode 1) stays on GB = 0 unless S3OD_RW_GB1=1: its grouped instance miscompiles under
-    // hipcc 7.2 (in-tile group stores dropped / masks misapplied; tools/rw_gb_diff.py)
-    const int gb = MODE == 1 && !S3OD_KNOB("S3OD_RW_GB1", 0) ? 0 : S3OD_KNOB("S3OD_RW_GB", 2);
+    // the masked data gradient (mode 1): GB 2 for 64 input channels; GB 4 miscompiles under hipcc 7.2 (in-tile group
+    // stores dropped / masks misapplied, tools/rw_gb_diff.py) and the 96-channel GB 2 instance spills, so those stay
+    // on GB 0 unless S3OD_RW_GB1=1 (dev)
+    int gb = S3OD_KNOB("S3OD_RW_GB", 2);
+    if (MODE == 1 && (CI == 96 || gb == 4) && !S3OD_KNOB("S3OD_RW_GB1", 0)) gb = 0;
     if (gb == 4) return launch_rw_g<MODE, CI, 4>(x, w, bias, res1, colsum, out, B, H, W, st, w2, b2, logits);
     if (gb == 2) return launch_rw_g<MODE, CI, 2>(x, w, bias, res1, colsum, out, B, H, W, st, w2, b2, logits);
   }

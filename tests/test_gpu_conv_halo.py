@@ -69,8 +69,8 @@ def test_conv_dgrad_relu_mask_and_colsum(cout_fwd):
 def test_rw_grouped_epilogue_bit_identical(gb):
     """The grouped epilogue (S3OD_RW_GB: each group's epilogue issued between the next group's MFMAs, the last group's
     carried into the next tile) runs the same MFMA chain per accumulator: outputs bit-identical to S3OD_RW_GB=0 for
-    the forward (bias + ReLU).  The masked 64 / 96-channel data gradients stay on GB = 0 (their grouped instance
-    miscompiles, S3OD_RW_GB1): checked unchanged under the knob; column sums to fp32 summation order."""
+    the forward (bias + ReLU) and the masked 64-channel data gradient at GB 2 (its GB 4 instance miscompiles and the
+    96-channel one spills: both stay on GB 0, checked unchanged under the knob); column sums to fp32 summation order."""
     from s3od_amd._lib import lib, stream
     B, H, W = 3, 37, 70                                    # ragged: partial tiles, several tiles per workgroup
     g = torch.Generator(device="cuda").manual_seed(11)

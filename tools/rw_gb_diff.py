@@ -26,6 +26,7 @@ def main():
         res1 = torch.randn(B, H, W, 64, device="cuda", generator=g).bfloat16()
         bias = torch.randn(64, device="cuda", generator=g) * 0.1
         outs = {}
+        os.environ["S3OD_RW_GB1"] = os.environ.get("GB1", "1")
         for k in ("0", gb):
             os.environ["S3OD_RW_GB"] = k
             dx = torch.full((B, H, W, 64), 7.0, device="cuda", dtype=torch.bfloat16)
@@ -35,9 +36,12 @@ def main():
             of = torch.full((B, H, W, 64), 7.0, device="cuda", dtype=torch.bfloat16)
             lib()("s3od_conv_fwd", BF16, B, H, W, 64, H, W, 64, 3, 3, 1, 1, x, 0, wp, bias, None, None, ACT_RELU, None, None,
                   of, None, None, None, stream())
+            o0 = torch.full((B, H, W, 64), 7.0, device="cuda", dtype=torch.bfloat16)
+            lib()("s3od_conv_fwd", BF16, B, H, W, 64, H, W, 64, 3, 3, 1, 1, x, 0, wp, bias, None, None, 0, None, None,
+                  o0, None, None, None, stream())
             torch.cuda.synchronize()
-            outs[k] = (dx, of, cs)
-        for i, nm in enumerate(("dgrad", "fwd")):
+            outs[k] = (dx, of, o0, cs)
+        for i, nm in enumerate(("dgrad", "fwd relu", "fwd plain")):
             a, b = outs[gb][i].float(), outs["0"][i].float()
             bad = (a != b).nonzero()
             print(f"B{B} H{H} W{W} {nm}: {bad.shape[0]} mismatches of {a.numel()}", flush=True)
@@ -47,7 +51,7 @@ def main():
                 for j in range(min(6, bad.shape[0])):
                     t = tuple(bad[j].tolist())
                     print("   ", t, float(a[t]), float(b[t]))
-        print("colsum maxdiff", float((outs[gb][2] - outs["0"][2]).abs().max()))
+        print("colsum maxdiff", float((outs[gb][3] - outs["0"][3]).abs().max()))
 
 
 if __name__ == "__main__":
