@@ -186,7 +186,9 @@ template <int CI> struct RwShape {
   static constexpr int ROWB = CI * 2, KK = CI / 32, NPC = TW / 16, PB = 4 * NPC;          // 16-px blocks per wave
   static constexpr int PIECES = ((PX * ROWB + 4095) / 4096) * 4, PPW = PIECES / 4;        // 1 KiB DMA pieces
   static constexpr int BUF = PIECES * 1024, LDS = 3 * BUF + 2048;       // + bias / column sums / head partials
-  static_assert(LDS <= 160 * 1024, "register-weight conv LDS budget");
+  // grouped mask heads: 3 tile slots of head partials [wave 4][row 4][block 2][head 3][lane 16] floats after that
+  static constexpr int PSLOT = 4 * 4 * 2 * 3 * 16, LDS_H = LDS + 3 * PSLOT * 4;
+  static_assert(LDS <= 160 * 1024 && (CI != 64 || LDS_H <= 160 * 1024), "register-weight conv LDS budget");
   // 16-B slot of logical chunk c in halo row px (an involution; conflict-free ds_read_b128 for every tap offset,
   // checked against the gfx950 lane groups): CI 64: c ^ (px & 7); CI 96: XOR of the low 2 bits, groups of 4 kept
   DEV static int slot(int c, int px) {
@@ -221,7 +223,7 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
   constexpr int PB = S::PB, PPW = S::PPW, NPC = S::NPC, HC = S::HC, ROWB = S::ROWB;
   constexpr int NB = MODE == 3 ? 3 : 2, CO = 32 * NB;     // 16-channel blocks per wave / output channels
   static_assert(MODE != 3 || (CI == 64 && NPC == 2), "mask heads: 64 input channels, 8 x 32 tiles");
-  static_assert(GB == 0 || (MODE != 3 && PB % GB == 0), "grouped epilogue: modes 0-2, whole groups");
+  static_assert(GB == 0 || (MODE != 3 && PB % GB == 0) || (MODE == 3 && GB == NPC), "grouped epilogue: whole groups (heads: one row)");
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int lr = lane & 15, lg = lane >> 4, odd = lg & 1;
@@ -328,6 +330,69 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
     for (int e = 0; e < 8; e++) ob[e] = (bf16)o[e];
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, ob), r, p, 0, 0);
   };
+  // MODE 3, grouped: a block's epilogue (h = ReLU(acc) -> hsave, the three head partials summed over the 4 lg lanes
+  // -> LDS slot `slot` [wave][row r][block c][head][lr]); the logits of tile t are stored two tiles later, after the
+  // per-tile barrier has made both waves' partials visible (3 slots: a slot is rewritten only after every wave has
+  // passed the barrier behind its reads), in the same summation order as the ungrouped path (bit-identical)
+  int cslot = 2, cgi = 0;                             // the carried group's partial slot / row (dummy: slot of tile -1)
+  float* pslots = (float*)(smem + 3 * S::BUF + 2048);
+  auto pix = [&](int slot, int w, int r, int c, int h, int l) { return ((((slot * 4 + w) * 4 + r) * 2 + c) * 3 + h) * 16 + l; };
+  auto epi_head = [&](const f32x4 (&a)[NB], unsigned p, int bbx, int slot, int r, int c) {
+    const auto rs = make_rsrc(out + bbx * img_o, out ? (unsigned long)img_o * 2 : 0ul);
+    float v[NB][4];
+#pragma unroll
+    for (int nb = 0; nb < NB; nb++)
+#pragma unroll
+      for (int e = 0; e < 4; e++) v[nb][e] = fmaxf(a[nb][e], 0.f);
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[0][e]), __float_as_uint(v[1][e]), false, false);
+      o[e] = __uint_as_float(sw[0]);
+      o[4 + e] = __uint_as_float(sw[1]);
+    }
+    bf16x8 ob;
+#pragma unroll
+    for (int e = 0; e < 8; e++) ob[e] = (bf16)o[e];
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, ob), rs, p, 0, 0);
+    if constexpr (NB == 3) {
+      const unsigned p2 = p == 0x80000000u ? p : p - cb * 2 + (ch0 + 32 + 4 * lg) * 2;
+      const bf16x4 o2 = {(bf16)v[2][0], (bf16)v[2][1], (bf16)v[2][2], (bf16)v[2][3]};
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, o2), rs, p2, 0, 0);
+    }
+#pragma unroll
+    for (int nb = 0; nb < NB; nb++) {
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; e++) d += v[nb][e] * aux[96 + ch0 + 16 * nb + 4 * lg + e];
+      d += __shfl_xor(d, 16);
+      d += __shfl_xor(d, 32);
+      if (lg == 0) pslots[pix(slot, wave, r, c, nb, lr)] = d;
+    }
+  };
+  auto store_logits = [&](int tt, bool valid, int slot) {
+    const int tc = valid ? tt : t_beg;
+    const int txi = tc % tiles_x, t2 = tc / tiles_x, tyi = t2 % tiles_y, bb = t2 / tiles_y;
+    const auto rl = make_rsrc(logits + (long)bb * 3 * H * W, (unsigned long)3 * H * W * 4);
+    const int c = lg & 1;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int gy = tyi * S::TH + row0 + r, gx = txi * S::TW + c * 16 + lr;
+      const bool ok = valid && lg < 2 && gy < H && gx < W;
+      const unsigned base = (unsigned)(gy * W + gx) * 4;
+      if (!(wave & 1)) {
+        const float l0 = aux[192] + pslots[pix(slot, wave, r, c, 0, lr)] + pslots[pix(slot, wave, r, c, 1, lr)];
+        const float l1 = aux[193] + pslots[pix(slot, wave, r, c, 2, lr)] + pslots[pix(slot, wave + 1, r, c, 0, lr)];
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(l0), rl, ok ? base : 0x80000000u, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(l1), rl, ok ? base + (unsigned)H * W * 4 : 0x80000000u, 0, 0);
+      } else {
+        const float l2 = aux[194] + pslots[pix(slot, wave, r, c, 1, lr)] + pslots[pix(slot, wave, r, c, 2, lr)];
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(l2), rl, ok ? base + 2u * H * W * 4 : 0x80000000u, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(0u, rl, 0x80000000u, 0, 0);   // keeps the per-tile store count uniform
+      }
+    }
+  };
+  (void)epi_head; (void)store_logits; (void)pix;
 
   int tile = t_beg + wi, k = 0;
   issue(tile, 0);
@@ -355,12 +420,14 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
     if (k == 0) { if constexpr (MODE == 1) wait_vmcnt<PPW + PB>(); else wait_vmcnt<PPW>(); }
     else if (k == 1) { if constexpr (MODE == 1) wait_vmcnt<PB + PPW + PB + PB>(); else wait_vmcnt<PPW + NS>(); }
     else { if constexpr (MODE == 1) wait_vmcnt<PB + PB + PPW + PB + PB>(); else wait_vmcnt<NS + PPW + NS>(); }
+    if constexpr (MODE == 3 && GB > 0) wait_lgkm0();  // this wave's head partials written before the barrier
     __builtin_amdgcn_s_barrier();                     // every wave's pieces landed; every wave done with slot k-1
     asm volatile("" ::: "memory");
     issue(tile + 2 * wpx, (k + 2) % 3);
     const char* hb = smem + (k % 3) * S::BUF;
     constexpr int NST = 9 * S::KK;
     if constexpr (GB > 0) {
+      if constexpr (MODE == 3) store_logits(tile - 2 * wpx, k >= 2, (k + 1) % 3);
       // fragments of group gi's GB blocks for step st; the group's MFMAs; the carried group's epilogue in the first
       // GB step pairs
       auto rd_g = [&](int gi, int st, bf16x8 (&fa)[GB]) {
@@ -394,7 +461,10 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
           if (st + 1 < NST) rd_g(gi, st + 1, fa1);
           __builtin_amdgcn_sched_barrier(0);
           mm_g(st, fa0);
-          if (st / 2 < GB) epi_blk(cacc[st / 2], cpo[st / 2], crm[st / 2], cbb);
+          if (st / 2 < GB) {
+            if constexpr (MODE == 3) epi_head(cacc[st / 2], cpo[st / 2], cbb, cslot, cgi, st / 2);
+            else epi_blk(cacc[st / 2], cpo[st / 2], crm[st / 2], cbb);
+          }
           __builtin_amdgcn_sched_barrier(0);
           if (st + 2 < NST) rd_g(gi, st + 2, fa0);
           __builtin_amdgcn_sched_barrier(0);
@@ -409,6 +479,8 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
           if constexpr (MODE == 1) crm[q] = rm_[gi * GB + q];
         }
         cbb = bb;
+        cslot = k % 3;
+        cgi = gi;
       }
       continue;
     }
@@ -518,8 +590,16 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
     }
   }
   if constexpr (GB > 0) {                             // the last tile's carried group
+    if constexpr (MODE == 3) {
 #pragma unroll
-    for (int q = 0; q < GB; q++) epi_blk(cacc[q], cpo[q], crm[q], cbb);
+      for (int q = 0; q < GB; q++) epi_head(cacc[q], cpo[q], cbb, cslot, cgi, q);
+      lds_barrier();                                  // the last two tiles' partials complete: store their logits
+      store_logits(tile - 2 * wpx, k >= 2, (k + 1) % 3);
+      store_logits(tile - wpx, k >= 1, (k + 2) % 3);
+    } else {
+#pragma unroll
+      for (int q = 0; q < GB; q++) epi_blk(cacc[q], cpo[q], crm[q], cbb);
+    }
   }
   if (MODE == 1 && colsum) {                          // 16 lanes (lr) -> 1, LDS atomics, one global add per channel
 #pragma unroll
@@ -543,13 +623,14 @@ static int launch_rw_g(const bf16* x, const bf16* w, const float* bias, const bf
                        int B, int H, int W, hipStream_t st, const float* w2, const float* b2, float* logits) {
   typedef RwShape<CI> S;
   auto kfn = conv3x3_c64_rw_kernel<MODE, CI, GB>;
-  static const bool attr = ((void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS), true);   // once per process (thread-safe static init)
+  constexpr int LDS = MODE == 3 && GB > 0 ? S::LDS_H : S::LDS;
+  static const bool attr = ((void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, LDS), true);   // once per process (thread-safe static init)
   (void)attr;
   const int tx = cdiv(W, S::TW), ty = cdiv(H, S::TH);
   const long tiles = (long)B * tx * ty;
   if (tiles >= (1L << 31)) { s3od_set_error("conv rw: too many tiles"); return 22; }
     const int nwg = (int)std::min<long>(std::max<long>(tiles, 8), (long)s3od_cu_count());   // one persistent WG per CU, >= 8 so every XCD owns its range
-  hipLaunchKernelGGL(kfn, dim3(nwg), dim3(256), S::LDS, st, x, w, bias, res1, colsum, out, H, W, tx, ty, (int)tiles, w2, b2,
+  hipLaunchKernelGGL(kfn, dim3(nwg), dim3(256), LDS, st, x, w, bias, res1, colsum, out, H, W, tx, ty, (int)tiles, w2, b2,
                      logits);
   return s3od_check_launch("conv3x3_c64_rw");
 }
@@ -560,7 +641,11 @@ template <int MODE, int CI>
 static int launch_rw(const bf16* x, const bf16* w, const float* bias, const bf16* res1, float* colsum, bf16* out,
                      int B, int H, int W, hipStream_t st, const float* w2 = nullptr, const float* b2 = nullptr,
                      float* logits = nullptr) {
-  if constexpr (MODE != 3) {
+  if constexpr (MODE == 3) {
+    // mask heads grouped by output row (S3OD_RW_HGB=2, opt-in): bit-identical but slower, 2160-2174 -> 2421-2424 us at
+    // bs 16 x 1024^2 (the weights' AGPR reads double the loop's VALU; profiles/r05t_rw_grouped_epilogue.txt)
+    if (S3OD_KNOB("S3OD_RW_HGB", 0) == 2) return launch_rw_g<3, CI, 2>(x, w, bias, res1, colsum, out, B, H, W, st, w2, b2, logits);
+  } else {
     // the masked data gradient (mode 1): GB 2 for 64 input channels; GB 4 miscompiles under hipcc 7.2 (in-tile group
     // stores dropped / masks misapplied, tools/rw_gb_diff.py) and the 96-channel GB 2 instance spills, so those stay
     // on GB 0 unless S3OD_RW_GB1=1 (dev)

@@ -111,6 +111,32 @@ def test_rw_grouped_epilogue_bit_identical(gb):
             assert float((a - b).abs().max()) <= 1e-4 * float(b.abs().max()) + 1e-3, i
 
 
+@pytest.mark.parametrize("B,H,W", [(2, 50, 41), (3, 37, 70)])
+def test_mask_heads_grouped_bit_identical(B, H, W):
+    """Mask heads with the grouped epilogue (S3OD_RW_HGB=2: logits stored two tiles later from LDS partial slots) vs
+    the ungrouped kernel (S3OD_RW_HGB=0): logits and hsave bit-identical (same summation order)."""
+    from s3od_amd._lib import lib, stream
+    g = torch.Generator(device="cuda").manual_seed(B * H + W)
+    feat = torch.randn(B, H, W, 64, device="cuda", generator=g).bfloat16()
+    w1 = (torch.randn(96, 3, 3, 64, device="cuda", generator=g) * 0.06).bfloat16()
+    b1 = torch.randn(96, device="cuda", generator=g) * 0.1
+    w2 = torch.randn(3, 32, device="cuda", generator=g) * 0.2
+    b2 = torch.randn(3, device="cuda", generator=g) * 0.1
+    outs = []
+    try:
+        for hgb in ("0", "2"):
+            os.environ["S3OD_RW_HGB"] = hgb
+            logits = torch.full((B, 3, H, W), 7.0, device="cuda")
+            hsave = torch.full((B * H * W, 96), 7.0, device="cuda", dtype=torch.bfloat16)
+            lib()("s3od_mask_heads_fwd", BF16, B, H, W, 3, feat, w1, b1, w2, b2, logits, hsave, stream())
+            torch.cuda.synchronize()
+            outs.append((logits, hsave))
+    finally:
+        os.environ.pop("S3OD_RW_HGB", None)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
 def test_mask_heads_fwd_halo():
     from s3od_amd._lib import lib, stream
     B, H, W, NM = 2, 50, 41, 3
