@@ -230,6 +230,7 @@ def test_c5_2048_bf16_vs_strict(model):
     assert rel_l2(b["pred_iou"], iou_s) <= 3e-2
 
 
+@pytest.mark.timeout(900)   # the oracle's fp32 2048^2 convs (MIOpen) can take minutes on a cold box
 def test_c5_one_image_strict_vs_oracle(model):
     from oracle import s3od_oracle as O
     x, _ = _batch(1, 2048, 52)
@@ -245,6 +246,7 @@ def test_c5_one_image_strict_vs_oracle(model):
 
 
 # ------------------------------------------------------------------------------------ bf16 vs the oracle
+@pytest.mark.timeout(900)   # the oracle's fp32 2048^2 convs (MIOpen) can take minutes on a cold box
 def test_bf16_vs_oracle_production_sizes(model):
     """The bf16 fast path checked against the ORACLE (not against the build's own f32 path) at the sizes the
     metric is quoted on: image 0 of a bs-8 1024^2 batch (C2) and of a bs-4 2048^2 batch (C5), and a bs-1
