@@ -32,31 +32,6 @@ def timeit(fn, n=5):
 def main():
     B = 16
     pmc = sys.argv[1:2] == ["pmc"]
-    if sys.argv[1:2] == ["dbg"]:                  # per-wave wall-clock split of the producer kernel (S3OD_WGD_DBG)
-        H, cin, cout = 1024, 64, 64
-        dy = torch.randn(B, H, H, cout, device="cuda").bfloat16()
-        x = torch.randn(B, H, H, cin, device="cuda").bfloat16()
-        ws = torch.zeros(cout * 9 * cin, device="cuda")
-        dw = torch.zeros(cout, cin, 3, 3, device="cuda")
-        buf = torch.zeros(4096 * 5 * 8, dtype=torch.int64, device="cuda")
-        f = lambda: lib()("s3od_conv_wgrad", BF16, B, H, H, cin, H, H, cout, 3, 3, 1, 1, dy, x, 0, dw, ws, 0, None, 0, stream())
-        if len(sys.argv) > 3:
-            os.environ[sys.argv[2]] = sys.argv[3]
-        t = timeit(f)
-        os.environ["S3OD_WGD_DBG"] = str(buf.data_ptr())
-        f()
-        torch.cuda.synchronize()
-        os.environ.pop("S3OD_WGD_DBG")
-        d = buf.view(-1, 5, 8).cpu().double()
-        d = d[d[:, 0, 5] > 0]
-        n = d[:, 0, 5:6]
-        print(f"{t * 1e6:.1f} us; {len(d)} workgroups, {float(n.mean()):.1f} tiles each (us per tile)")
-        for w in range(5):
-            e = d[:, w] / 100
-            nm = ("compute", "barrier", "-") if w < 4 else ("vmwait", "barrier", "issue")
-            print(f"  wave {w}: {nm[0]} {float((e[:, 0] / n[:, 0]).mean()):.3f} {nm[1]} {float((e[:, 1] / n[:, 0]).mean()):.3f}"
-                  f" {nm[2]} {float((e[:, 2] / n[:, 0]).mean()):.3f}  span {float((e[:, 4] - e[:, 3]).mean()):.1f} us")
-        return
     if sys.argv[1:2] == ["big"]:                  # the 256-channel RCU / layerK_rn weight gradients: ping-pong (DMA=0) vs LDS-DMA
         for (H, cin, cout, relu) in ((256, 256, 256, 0), (256, 256, 256, 1), (128, 256, 256, 0), (128, 512, 256, 0),
                                      (64, 256, 256, 0), (64, 1024, 256, 0)):
@@ -111,7 +86,7 @@ def main():
         res = {}
         for rnd in range(1 if pmc else 3):
             for knob in ("1",) if pmc else ("0", "1", "p0"):
-                os.environ["S3OD_WGRAD_DMA"] = knob[-1]
+                os.environ["S3OD_WGRAD_DMA"] = "0" if knob == "0" else "1"   # p0: the 4-wave LDS-DMA kernel
                 os.environ["S3OD_WGD_PROD"] = "0" if knob == "p0" else "1"
                 dw = torch.zeros(cout, cin, 3, 3, device="cuda")
                 f = lambda: lib()("s3od_conv_wgrad", BF16, B, H, H, cin, H, H, cout, 3, 3, 1, 1, dy, x, relu, dw, ws, 0, None, 0, stream())
