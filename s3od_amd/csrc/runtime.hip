@@ -26,6 +26,6 @@ extern "C" {
 
 const char* s3od_last_error(void) { return g_err; }
 
-int s3od_abi_version(void) { return 1; }
+int s3od_abi_version(void) { return 2; }   // 2: s3od_colsum takes a partial-sum workspace (+ s3od_colsum_ws)
 
 }  // extern "C"

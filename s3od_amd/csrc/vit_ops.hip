@@ -252,10 +252,11 @@ __global__ void cast_tap_kernel(const float* __restrict__ x, T* __restrict__ y, 
 
 // column sums of a [M, N] T matrix (bias gradients): out[n] += sum_m a[m, n]
 // block = 256 threads = tpr column-groups (8 columns each) x rp row phases; LDS reduction over
-// the row phases, one fp32 atomic per column per block.
+// the row phases, then per block either one fp32 atomic per column (part == nullptr) or the block's partial
+// sums stored to part[blockIdx.y][N] for colsum_fold_kernel.
 template <typename T>
 __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ a, long lda, int M, int N, float* __restrict__ out,
-                                                     int rows_per_block) {
+                                                     int rows_per_block, float* __restrict__ part) {
   __shared__ float red[256 * 8];
   const int G = N / 8;
   const int tpr = G < 256 ? G : 256, rp = 256 / tpr;
@@ -287,8 +288,40 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ a, lo
     for (int q = 1; q < rp; q++)
 #pragma unroll
       for (int e = 0; e < 8; e++) s[e] += red[(q * tpr + ci) * 8 + e];
+    if (part) {
+      float* pr = part + (long)blockIdx.y * N + cg * 8;
+      *(float4*)pr = make_float4(s[0], s[1], s[2], s[3]);
+      *(float4*)(pr + 4) = make_float4(s[4], s[5], s[6], s[7]);
+    } else {
 #pragma unroll
-    for (int e = 0; e < 8; e++) atomicAdd(out + cg * 8 + e, s[e]);
+      for (int e = 0; e < 8; e++) atomicAdd(out + cg * 8 + e, s[e]);
+    }
+  }
+}
+// out[n] += sum over the nb partial rows in a fixed order (deterministic): block = 32 columns x 8 row groups, each
+// thread sums rows rg, rg + 8, ... with 8 loads in flight, then the 8 group sums are added in group order
+__global__ void __launch_bounds__(256) colsum_fold_kernel(const float* __restrict__ part, int nb, int N, float* __restrict__ out) {
+  __shared__ float red[8][32];
+  const int c = threadIdx.x & 31, rg = threadIdx.x >> 5, n = blockIdx.x * 32 + c;
+  float s = 0.f;
+  if (n < N) {
+    int r = rg;
+    for (; r + 56 < nb; r += 64) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) v[u] = part[(long)(r + 8 * u) * N + n];
+#pragma unroll
+      for (int u = 0; u < 8; u++) s += v[u];
+    }
+    for (; r < nb; r += 8) s += part[(long)r * N + n];
+  }
+  red[rg][c] = s;
+  __syncthreads();
+  if (rg == 0 && n < N) {
+    float t = red[0][c];
+#pragma unroll
+    for (int q = 1; q < 8; q++) t += red[q][c];
+    out[n] += t;
   }
 }
 
@@ -477,14 +510,33 @@ int s3od_cast_tap(int dtype, const float* x, void* y, int B, int Ntok, int P, in
   return s3od_check_launch("cast_tap");
 }
 
-int s3od_colsum(int dtype, const void* a, long lda, int M, int N, float* out, void* stream) {
+// row blocks of the column sum: <= ~512 of >= 64 rows.  Without a workspace each block adds its sums by fp32
+// atomics, which serialise on one address in L2: 256 / 512 / 1024 of them cost ~50 / 100 / 200 us whatever the
+// matrix size (tools/colsum_bench.py, profiles/r05w_colsum.txt); with one, the blocks store partial rows and a
+// second pass adds them in a fixed order
+static long colsum_rpb(int M, int gx, bool ws) { (void)ws; return max(64L, (long)M * gx / 512); }
+// bytes of the partial-sum workspace s3od_colsum uses for these arguments
+int s3od_colsum_ws(int M, int N, long* bytes) {
+  S3OD_REQUIRE(bytes != nullptr && N % 8 == 0, "colsum_ws: bad arguments");
+  const int G = N / 8, tpr = G < 256 ? G : 256, gx = cdiv(G, tpr);
+  *bytes = 4L * cdiv(M, colsum_rpb(M, gx, true)) * N;
+  return 0;
+}
+
+int s3od_colsum(int dtype, const void* a, long lda, int M, int N, float* out, float* ws, long ws_bytes, void* stream) {
   S3OD_REQUIRE(N % 8 == 0, "colsum: N %% 8");
   const int G = N / 8, tpr = G < 256 ? G : 256, gx = cdiv(G, tpr);
-  long rpb = max(64L, (long)M * gx / 512);   // <= ~512 fp32 atomics per address (contention)
-  dim3 grid(gx, cdiv(M, rpb));
+  long need = 0;
+  if (ws) s3od_colsum_ws(M, N, &need);
+  const bool two_pass = ws && ws_bytes >= need && N % 4 == 0 && !S3OD_OFF("S3OD_COLSUM_2P");
+  const long rpb = colsum_rpb(M, gx, two_pass);
+  const int nb = (int)cdiv(M, rpb);
+  dim3 grid(gx, nb);
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL(colsum_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)a, lda, M, N, out, (int)rpb);
+    hipLaunchKernelGGL(colsum_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)a, lda, M, N, out, (int)rpb,
+                       two_pass ? ws : nullptr);
   });
+  if (two_pass) hipLaunchKernelGGL(colsum_fold_kernel, dim3(cdiv(N, 32)), dim3(256), 0, (hipStream_t)stream, ws, nb, N, out);
   return s3od_check_launch("colsum");
 }
 

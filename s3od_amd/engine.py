@@ -463,7 +463,17 @@ class DPTEngine:
 
     # ================================================================== backward
     def _colsum(self, a, M, N, out, lda=None):
-        lib()("s3od_colsum", self.dt, a, lda or N, M, N, out, stream())
+        """Bias gradient out += column sums of a [M, N]: two fixed-order passes through a caller-owned partial-sum
+        buffer (the library's own size query; allocated on the calling stream, so the caching allocator orders its
+        reuse behind this stream)."""
+        key = ("colsum", M, N)
+        nb = self._slab_need.get(key)
+        if nb is None:
+            n = ctypes.c_long(0)
+            lib()("s3od_colsum_ws", M, N, ctypes.addressof(n))
+            nb = self._slab_need[key] = int(n.value)
+        ws = torch.empty(max(nb // 4, 1), dtype=torch.float32, device=out.device)
+        lib()("s3od_colsum", self.dt, a, lda or N, M, N, out, ws, nb, stream())
 
     def _slab(self, entry, key, *args):
         """Caller-owned split-K slab workspace for a weight-gradient entry (the C ABI never allocates): sized by the

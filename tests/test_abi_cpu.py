@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     raw = ctypes.CDLL(str(LIB_PATH))
     for name in L.decls:
         assert hasattr(raw, name), name
-    assert L.lib.s3od_abi_version() == 1
+    assert L.lib.s3od_abi_version() == 2
     # every declared arg type maps to a ctypes type
     for name, (ret, types) in L.decls.items():
         assert len(L.fns[name][0].argtypes) == len(types)

@@ -27,6 +27,7 @@ REF = {
     "s3od_layernorm_bwd": "LayerNorm backward (reference: implicit torch autograd)",
     "s3od_cast_tap": "hidden_states[2,5,8,11] (dinob) / [4,11,17,23] (dinol) [:, 1+4:] taps: src/s3od/model.py:62-86, MT/model.py:28-32",
     "s3od_colsum": "bias gradients (reference: implicit torch autograd)",
+    "s3od_colsum_ws": "workspace query of s3od_colsum: bytes of the caller-owned partial-sum buffer (new; torch autograd reduces internally)",
     "s3od_layerscale_bwd": "DINOv3ViTLayerScale backward: tf:modeling_dinov3_vit.py:337-343",
     "s3od_qkv_unrope": "apply_rotary_pos_emb backward: tf:modeling_dinov3_vit.py:238-268",
     "s3od_repack_weight": "weight layout for the kernels (the reference's state_dict layout is kept for params)",
@@ -75,6 +76,7 @@ WS = {
     "s3od_attn_bwd_qkv": "ws: fp32 [S3OD_NREP][2][64 H], all zero on entry, left all zero",
     "s3od_conv_wgrad": "ws (nullable): fp32 [Cout][KH][KW][Cin], all zero on entry, left all zero; slab (nullable): >= s3od_conv_wgrad_ws bytes, contents dead between calls",
     "s3od_avgpool": "ws: fp32 [B][ceil(HW / 1024)][C] partial sums, contents dead between calls (a fixed-order two-pass mean: deterministic)",
+    "s3od_colsum": "ws (nullable): >= s3od_colsum_ws bytes of fp32 partial sums, contents dead between calls (with it the sum is two fixed-order passes: deterministic, no same-address atomics; without it one fp32 atomic per column per block)",
     "s3od_linear_wgrad": "slab (nullable): >= s3od_linear_wgrad_ws bytes, contents dead between calls (without it the split-K partials are fp32 atomics into dw)",
 }
 
