@@ -1012,10 +1012,11 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __r
   __syncthreads();
   // the tile loop is unrolled by two so the LDS stage is a compile-time constant (every fragment address
   // becomes a per-lane base + immediate instead of being recomputed from the stage index each tile)
-  auto tile = [&](int qt, auto CUR) {
-    constexpr int cur = decltype(CUR)::value;
-    if (qt + 1 < nqt) stage(qt + 1, smem + (cur ^ 1) * SB);
-    const char* qs_ = smem + cur * SB;
+  // the stage pointers are __restrict__ parameters: the noalias scopes they carry after inlining let the
+  // compiler's wait-count pass see that this tile's LDS reads cannot alias the next tile's LDS-DMA (without
+  // them it put a vmcnt(0) before the first transposed read of every tile, waiting out the prefetch)
+  auto tile = [&](int qt, char* __restrict__ nxt, const char* __restrict__ qs_) {
+    if (qt + 1 < nqt) stage(qt + 1, nxt);
     const char* dos = qs_ + Img32::BYTES;
     const float* lsel = (const float*)(qs_ + 2 * Img32::BYTES);
     const float* dll = (const float*)(qs_ + 2 * Img32::BYTES + 1024);
@@ -1067,8 +1068,8 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dkdv32_kernel(const bf16* __r
     __syncthreads();      // drains this tile's reads and the next tile's LDS-DMA (vmcnt(0)) before the flip
   };
   int qt = 0;
-  for (; qt + 1 < nqt; qt += 2) { tile(qt, std::integral_constant<int, 0>{}); tile(qt + 1, std::integral_constant<int, 1>{}); }
-  if (qt < nqt) tile(qt, std::integral_constant<int, 0>{});
+  for (; qt + 1 < nqt; qt += 2) { tile(qt, smem + SB, smem); tile(qt + 1, smem, smem + SB); }
+  if (qt < nqt) tile(qt, smem + SB, smem);
   if (sink.dqkv) {
     float csk[2] = {0.f, 0.f}, csv[2] = {0.f, 0.f};
     qkv_sink32<bf16>(sink, 1, b, hh, H, k0, N, lane, dk, -LN2, csk);
@@ -1131,10 +1132,8 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __res
   };
   stage(0, smem);
   __syncthreads();
-  auto tile = [&](int kt, auto CUR) {      // unrolled by two, as in the dK/dV pass
-    constexpr int cur = decltype(CUR)::value;
-    if (kt + 1 < nkt) stage(kt + 1, smem + (cur ^ 1) * SB);
-    const char* ks_ = smem + cur * SB;
+  auto tile = [&](int kt, char* __restrict__ nxt, const char* __restrict__ ks_) {   // unrolled by two, as in the dK/dV pass
+    if (kt + 1 < nkt) stage(kt + 1, nxt);
     const char* vs_ = ks_ + Img32::BYTES;
     f32x16 s[2], dp[2];
     bf16x8 da[2][2];
@@ -1183,8 +1182,8 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __res
     __syncthreads();
   };
   int kt = 0;
-  for (; kt + 1 < nkt; kt += 2) { tile(kt, std::integral_constant<int, 0>{}); tile(kt + 1, std::integral_constant<int, 1>{}); }
-  if (kt < nkt) tile(kt, std::integral_constant<int, 0>{});
+  for (; kt + 1 < nkt; kt += 2) { tile(kt, smem + SB, smem); tile(kt + 1, smem, smem + SB); }
+  if (kt < nkt) tile(kt, smem + SB, smem);
   if (sink.dqkv) {
     float csq[2] = {0.f, 0.f};
     qkv_sink32<bf16>(sink, 0, b, hh, H, q0, N, lane, dq, -0.125f, csq);

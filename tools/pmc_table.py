@@ -30,6 +30,18 @@ def main():
             print(f"   {c:28s} {v:16.5g}")
         if m.get("SQ_INSTS_MFMA"):
             print(f"   {'(VALU-MFMA)/MFMA':28s} {(m.get('SQ_INSTS_VALU', 0) - m['SQ_INSTS_MFMA']) / m['SQ_INSTS_MFMA']:16.3f}")
+        wc = m.get("SQ_WAVE_CYCLES")
+        if wc:
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
+                if c in m:
+                    print(f"   {c + ' / WAVE_CYCLES':28s} {m[c] / wc:16.3f}")
+            if m.get("GRBM_GUI_ACTIVE"):
+                # SQ_WAVE_CYCLES is in quad-cycles summed over waves; GRBM_GUI_ACTIVE sums 8 XCDs
+                print(f"   {'waves per SIMD (avg)':28s} {wc * 4 / (m['GRBM_GUI_ACTIVE'] / 8 * 1024):16.3f}")
+        if m.get("SQ_INSTS_MFMA") and m.get("SQ_INSTS_LDS"):
+            print(f"   {'LDS insts / MFMA':28s} {m['SQ_INSTS_LDS'] / m['SQ_INSTS_MFMA']:16.3f}")
+        if m.get("SQ_LDS_IDX_ACTIVE") and m.get("GRBM_GUI_ACTIVE"):
+            print(f"   {'LDS busy / CU-cycle':28s} {m['SQ_LDS_IDX_ACTIVE'] / (m['GRBM_GUI_ACTIVE'] / 8 * 256):16.3f}")
         if m.get("SQ_BUSY_CYCLES") and m.get("SQ_VALU_MFMA_BUSY_CYCLES") and m.get("GRBM_GUI_ACTIVE"):
             # GRBM_GUI_ACTIVE sums the 8 XCDs; MFMA busy cycles sum 256 CUs x 4 SIMDs
             cyc = m["GRBM_GUI_ACTIVE"] / 8
