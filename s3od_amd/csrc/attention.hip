@@ -308,8 +308,15 @@ __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(const T* __restrict__ 
   if constexpr (!F32) {
     if (fast) {
       run(std::true_type{});
-      // the rare overflow of the fixed-max path: rerun the block with the lazy rescale
-      const bool bad = !(lacc[0][0] < 3.0e38f) || !(lacc[1][0] < 3.0e38f);
+      // the rare overflow of the fixed-max path: rerun the block with the lazy rescale.  O overflows first when
+      // |V| > 1 (l just under FLT_MAX times |v| > FLT_MAX), so the accumulators are checked too (once per block).
+      bool bad = !(lacc[0][0] < 3.0e38f) || !(lacc[1][0] < 3.0e38f);
+#pragma unroll
+      for (int ds = 0; ds < 4; ds++)
+#pragma unroll
+        for (int qs = 0; qs < 2; qs++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) bad |= !(fabsf(o[ds][qs][i]) < 3.0e38f);
       if (__syncthreads_or(bad)) run(std::false_type{});
     } else {
       run(std::false_type{});

@@ -204,7 +204,7 @@ template <int CI> struct RwShape {
 // Every wave issues a FIXED sequence of vector-memory instructions per tile (PPW DMA pieces, PB mask loads, PB stores:
 // dummy pieces / out-of-image lanes use an out-of-range buffer offset instead of a branch), so the counted vmcnt
 // that retires a tile's halo is a per-phase constant.
-// GB > 0 (MODE 0-2): the tile's PB blocks run in groups of GB (all 9 * KK steps of one group's GB x NB accumulators,
+// GB > 0 (MODE 0 / 2; mode 1 is launched ungrouped, see launch_rw): the tile's PB blocks run in groups of GB (all 9 * KK steps of one group's GB x NB accumulators,
 // then the next group's), and each group's epilogue (ReLU / mask, lane-pair trade, pack, store) is issued between the
 // NEXT group's MFMAs -- the last group's carried into the next tile's first group (a dummy group with out-of-range
 // stores before the first tile) -- so with one wave per SIMD the matrix pipe no longer idles through the epilogue.
@@ -305,8 +305,8 @@ __global__ void __launch_bounds__(256, 1) conv3x3_c64_rw_kernel(const bf16* __re
   // epilogue of one 16-px block: lane holds out[px = block, lr][co = ch0 + 16 nb + 4 lg .. +3]; v_permlane16_swap
   // trades rows 1 / 3 of the first operand with rows 0 / 2 of the second (row = 16 lanes = one lg): the even lg keeps
   // its nb 0 and receives the odd partner's nb 0, the odd lg keeps nb 1 and receives the even's -> channels cb .. cb+7
-  // (the output descriptor is built here from the batch index: a descriptor carried across tiles in SGPRs lost its
-  // range word under hipcc 7.2 -- the mode-1 instance's in-tile group stores were dropped)
+  // (the output descriptor is built here from the batch index: in a round-5 build a descriptor carried across tiles
+  // in SGPRs lost its range word in the grouped mode-1 instance, whose in-tile group stores were dropped)
   auto epi_blk = [&](const f32x4 (&a)[NB], unsigned p, u32x4v mraw, int bbx) {
     const auto r = make_rsrc(out + bbx * img_o, out ? (unsigned long)img_o * 2 : 0ul);
     float o[8];
@@ -634,9 +634,14 @@ static int launch_rw_g(const bf16* x, const bf16* w, const float* bias, const bf
                      logits);
   return s3od_check_launch("conv3x3_c64_rw");
 }
-// modes 0-2: the grouped epilogue (S3OD_RW_GB = blocks per group: 2 default, 4, or 0 = the epilogue after all MFMAs).
-// Measured (tools/conv64_bench.py, bs 16 x 1024^2 64 -> 64 + ReLU, same box): GB 0 1290-1309 us, GB 2 1225-1242,
-// GB 4 1251-1280 (profiles/r05t_rw_grouped_epilogue.txt)
+// modes 0 / 2 (forward): the grouped epilogue (S3OD_RW_GB = blocks per group: 2 default, or 0 = the epilogue after all
+// MFMAs).  Measured (tools/conv64_bench.py, bs 16 x 1024^2 64 -> 64 + ReLU, same box): GB 0 1290-1309 us, GB 2 1225-1242,
+// GB 4 1251-1280 (profiles/r05t_rw_grouped_epilogue.txt; GB 4 removed in round 6).
+// Mode 1 (the ReLU'-masked data gradient) runs ungrouped: its grouped instances were the only register-weight convs
+// that spill (GB 2: 62 SGPRs into VGPR lanes + 6 VGPRs into AGPRs; GB 4: 40 + 16), and GB 4 produced wrong outputs
+// (in-tile group stores dropped / masks misapplied) although its vector-memory order matches the hand-counted waits
+// (ISA audit); GB 2 saved only 60-110 us per step.  tests/test_kernel_resources_cpu.py keeps every
+// counted-vmcnt production kernel free of scratch and VGPR spills.
 template <int MODE, int CI>
 static int launch_rw(const bf16* x, const bf16* w, const float* bias, const bf16* res1, float* colsum, bf16* out,
                      int B, int H, int W, hipStream_t st, const float* w2 = nullptr, const float* b2 = nullptr,
@@ -645,14 +650,8 @@ static int launch_rw(const bf16* x, const bf16* w, const float* bias, const bf16
     // mask heads grouped by output row (S3OD_RW_HGB=2, opt-in): bit-identical but slower, 2160-2174 -> 2421-2424 us at
     // bs 16 x 1024^2 (the weights' AGPR reads double the loop's VALU; profiles/r05t_rw_grouped_epilogue.txt)
     if (S3OD_KNOB("S3OD_RW_HGB", 0) == 2) return launch_rw_g<3, CI, 2>(x, w, bias, res1, colsum, out, B, H, W, st, w2, b2, logits);
-  } else {
-    // the masked data gradient (mode 1): GB 2 for 64 input channels; GB 4 miscompiles under hipcc 7.2 (in-tile group
-    // stores dropped / masks misapplied, tools/rw_gb_diff.py) and the 96-channel GB 2 instance spills, so those stay
-    // on GB 0 unless S3OD_RW_GB1=1 (dev)
-    int gb = S3OD_KNOB("S3OD_RW_GB", 2);
-    if (MODE == 1 && (CI == 96 || gb == 4) && !S3OD_KNOB("S3OD_RW_GB1", 0)) gb = 0;
-    if (gb == 4) return launch_rw_g<MODE, CI, 4>(x, w, bias, res1, colsum, out, B, H, W, st, w2, b2, logits);
-    if (gb == 2) return launch_rw_g<MODE, CI, 2>(x, w, bias, res1, colsum, out, B, H, W, st, w2, b2, logits);
+  } else if constexpr (MODE != 1) {
+    if (S3OD_KNOB("S3OD_RW_GB", 2) == 2) return launch_rw_g<MODE, CI, 2>(x, w, bias, res1, colsum, out, B, H, W, st, w2, b2, logits);
   }
   return launch_rw_g<MODE, CI, 0>(x, w, bias, res1, colsum, out, B, H, W, st, w2, b2, logits);
 }
@@ -1773,10 +1772,16 @@ static bool wgrad_dma_ok(int dtype, int H, int W, int Cin, int OH, int OW, int C
          (long)H * W * (Cin > Cout ? Cin : Cout) * 2 < (1L << 31) && !S3OD_OFF("S3OD_WGRAD_DMA");
 }
 
+// the routing decision shared by the slab query and the call (the query ignored S3OD_WGRAD_HALO, so with
+// the knob off the call took the ping-pong path without the slab it needed)
+static bool wgrad_takes_dma(int dtype, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW, int stride, int pad) {
+  return S3OD_KNOB("S3OD_WGRAD_HALO", 1) && wgrad_dma_ok(dtype, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad);
+}
+
 int s3od_conv_wgrad_ws(int dtype, int B, int H, int W, int Cin, int OH, int OW, int Cout, int KH, int KW, int stride,
                        int pad, int split, long* bytes) {
   S3OD_REQUIRE(bytes != nullptr, "conv_wgrad_ws: null output");
-  const int sp = slab_ok() && !wgrad_dma_ok(dtype, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad)
+  const int sp = slab_ok() && !wgrad_takes_dma(dtype, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad)
                      ? conv_wgrad_pp_split(dtype, B, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad, split) : 0;
   *bytes = sp > 1 ? 4L * sp * Cout * KH * KW * Cin : 0;
   return 0;
@@ -1811,7 +1816,7 @@ int s3od_conv_wgrad(int dtype, int B, int H, int W, int Cin, int OH, int OW, int
   // the LDS-DMA kernel works on 64 x 64 channel blocks; the 96-output-channel mask heads (Cin 64) run as two output
   // blocks, the second reading 32 channels past each pixel's 96 (finite data of the next pixel, zeros past the image)
   // whose products are never flushed
-  const bool dma = wg_knob && ws && wgrad_dma_ok(dtype, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad);
+  const bool dma = ws && wgrad_takes_dma(dtype, H, W, Cin, OH, OW, Cout, KH, KW, stride, pad);
   if (dma || (wg_knob && dtype == S3OD_BF16 && ws && KH == 3 && KW == 3 && stride == 1 && pad == 1 && OH == H && OW == W &&
               Cin % 64 == 0 && coblk && (Cin == 64 || (long)H * W >= 512L * 512))) {
     int rc = dma ? wgrad3x3_dma_launch(relu_x, (const bf16*)dy, (const bf16*)x, ws, B, H, W, Cin, Cout, st) :

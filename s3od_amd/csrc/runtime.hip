@@ -26,6 +26,11 @@ extern "C" {
 
 const char* s3od_last_error(void) { return g_err; }
 
-int s3od_abi_version(void) { return 2; }   // 2: s3od_colsum takes a partial-sum workspace (+ s3od_colsum_ws)
+// ABI version 2 (round 5) changed these signatures against version 1:
+//   s3od_colsum         + float* ws, long ws_bytes   (caller-owned partial-sum buffer; new query s3od_colsum_ws)
+//   s3od_avgpool        + float* ws                  (per-block partials, deterministic two-pass sum)
+//   s3od_linear_wgrad   + float* slab, long slab_bytes (split-K slabs; new query s3od_linear_wgrad_ws)
+//   s3od_conv_wgrad     + float* slab, long slab_bytes (split-K slabs; new query s3od_conv_wgrad_ws)
+int s3od_abi_version(void) { return 2; }
 
 }  // extern "C"

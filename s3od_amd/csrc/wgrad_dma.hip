@@ -82,7 +82,7 @@ conv3x3_wgrad_dma_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x
 #pragma unroll
   for (int j = 0; j < HPW; j++) {
     const int row = (wave * HPW + j) * 8 + l8, hy = row / HT_HC, hx = row - hy * HT_HC;
-    hlo[j] = row < HT_PX ? (unsigned)(((hy * W + hx) * CinT) * 2 + ch * 16) : 0x80000000u;
+    hlo[j] = row < HT_PX ? (unsigned)(((hy * W + hx) * CinT) * 2 + ch * 16) : BUF_OOB;
     const unsigned code = (hy == 0 ? 1u : 0u) | (hy == HT_HR - 1 ? 2u : 0u) | (hx == 0 ? 4u : 0u) | (hx == HT_HC - 1 ? 8u : 0u);
     hcode[j / 8] |= code << (4 * (j % 8));
   }
@@ -107,7 +107,7 @@ conv3x3_wgrad_dma_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x
     } else {
 #pragma unroll
       for (int j = 0; j < HPW; j++)
-        blds16(rx, ((hcode[j / 8] >> (4 * (j % 8))) & m) ? 0x80000000u : hlo[j], hd + j * 1024);
+        blds16(rx, ((hcode[j / 8] >> (4 * (j % 8))) & m) ? BUF_OOB : hlo[j], hd + j * 1024);
     }
   };
   // per-lane fragment bases (lane (g, l): u = 4 g + l / 4 its first K row, p = l % 4 its 4-column group), per ring slot
@@ -184,7 +184,7 @@ conv3x3_wgrad_dmap_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ 
 #pragma unroll
     for (int j = 0; j < HPP; j++) {
       const int row = (pw + NPROD * j) * 8 + l8, hy = row / HT_HC, hx = row - hy * HT_HC;
-      hlo[j] = row < HT_PX ? (unsigned)(((hy * W + hx) * CinT) * 2 + ch * 16) : 0x80000000u;
+      hlo[j] = row < HT_PX ? (unsigned)(((hy * W + hx) * CinT) * 2 + ch * 16) : BUF_OOB;
       const unsigned code = (hy == 0 ? 1u : 0u) | (hy == HT_HR - 1 ? 2u : 0u) | (hx == 0 ? 4u : 0u) | (hx == HT_HC - 1 ? 8u : 0u);
       hcode[j / 8] |= code << (4 * (j % 8));
     }
@@ -205,7 +205,7 @@ conv3x3_wgrad_dmap_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ 
       // halo pieces first: under a ReLU'd input the producers rectify the halo while the dy pieces still land
 #pragma unroll
       for (int j = 0; j < HPP; j++)
-        blds16(rx, ((hcode[j / 8] >> (4 * (j % 8))) & m) ? 0x80000000u : hlo[j], hd + (pw + NPROD * j) * 1024);
+        blds16(rx, ((hcode[j / 8] >> (4 * (j % 8))) & m) ? BUF_OOB : hlo[j], hd + (pw + NPROD * j) * 1024);
 #pragma unroll
       for (int j = 0; j < DPP; j++) {
         const int p = pw + NPROD * j;

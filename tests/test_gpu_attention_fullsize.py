@@ -141,10 +141,13 @@ def test_attn_bwd_qkv_fused_equals_separate_path():
         assert float((x - y).abs().max() / x.abs().max()) < 1e-2
 
 
-def test_attention_fwd_fixed_max_overflow_falls_back():
+@pytest.mark.parametrize("case", ["row_sum", "output"])
+def test_attention_fwd_fixed_max_overflow_falls_back(case):
     """The bf16 forward takes the row max over the first 64 keys only (S3OD_ATTN_FAST): a key whose score exceeds it by
-    more than the fp32 exponent range (here ~290 log2 units) overflows that pass, and the workgroup must rerun the block
-    with the lazy-rescale loop.  Output and LSE vs fp32 softmax, the planted row included."""
+    more than the fp32 exponent range overflows that pass, and the workgroup must rerun the block with the
+    lazy-rescale loop.  row_sum: ~290 log2 units above, the row sum itself overflows.  output: 123 log2
+    units above with |v| = 64 at that key -- the row sum stays under FLT_MAX (2^123) but P.V does not (2^129), which the
+    row-sum test alone missed.  Output and LSE vs fp32 softmax, the planted row included."""
     from s3od_amd._lib import lib, stream, BF16
     B, H, N = 1, 2, 1000
     g = torch.Generator(device="cuda").manual_seed(21)
@@ -152,9 +155,15 @@ def test_attention_fwd_fixed_max_overflow_falls_back():
     k = torch.randn(B * H, N, 64, device="cuda", generator=g)
     v = torch.randn(B * H, N, 64, device="cuda", generator=g)
     q[:, 5] = 0.0
-    q[:, 5, 0] = 40.0            # query 5 of every head ...
     k[:, 700] = 0.0
-    k[:, 700, 0] = 40.0          # ... meets key 700 (tile 10) with score 40 * 40 / 8 = 200 (natural units)
+    if case == "row_sum":
+        q[:, 5, 0] = 40.0        # query 5 of every head ...
+        k[:, 700, 0] = 40.0      # ... meets key 700 (tile 10) with score 40 * 40 / 8 = 200 (natural units)
+    else:
+        k[:, :, 0] = 0.0         # every other score of query 5 is exactly 0: m0 = 0
+        q[:, 5, 0] = 26.0
+        k[:, 700, 0] = 26.25     # score 26 * 26.25 / 8 = 85.3 natural = 123 log2 units: l ~ 2^123 < FLT_MAX
+        v[:, 700] = 64.0         # P.V ~ 2^129 > FLT_MAX
     q, k, v = q.bfloat16(), k.bfloat16(), v.bfloat16()
     qs = (q.float() * (LOG2E * 0.125)).bfloat16()
     o = torch.empty(B, N, H * 64, dtype=torch.bfloat16, device="cuda")

@@ -65,12 +65,12 @@ def test_conv_dgrad_relu_mask_and_colsum(cout_fwd):
     assert float((cs - ref_cs).abs().max()) <= float(tol), (float((cs - ref_cs).abs().max()), float(tol))
 
 
-@pytest.mark.parametrize("gb", ["2", "4"])
+@pytest.mark.parametrize("gb", ["2"])
 def test_rw_grouped_epilogue_bit_identical(gb):
     """The grouped epilogue (S3OD_RW_GB: each group's epilogue issued between the next group's MFMAs, the last group's
-    carried into the next tile) runs the same MFMA chain per accumulator: outputs bit-identical to S3OD_RW_GB=0 for
-    the forward (bias + ReLU) and the masked 64-channel data gradient at GB 2 (its GB 4 instance miscompiles and the
-    96-channel one spills: both stay on GB 0, checked unchanged under the knob); column sums to fp32 summation order."""
+    carried into the next tile) runs the same MFMA chain per accumulator: forward outputs (bias + ReLU) bit-identical
+    to S3OD_RW_GB=0.  The masked data gradients (64 and 96 input channels) run ungrouped whatever the knob (their
+    grouped instances spilled): checked unchanged under it; column sums to fp32 summation order."""
     from s3od_amd._lib import lib, stream
     B, H, W = 3, 37, 70                                    # ragged: partial tiles, several tiles per workgroup
     g = torch.Generator(device="cuda").manual_seed(11)

@@ -142,7 +142,6 @@ def _grad_report(grads, sd):
     return worst_n, worst_c
 
 
-@pytest.mark.timeout(900)
 def test_c3_multi_image_train_step_vs_oracle_1024():
     """A MULTI-image production-size train step (bs 2 at 1024^2: multi-image BN batch statistics, the M = 2 * 4101
     GEMM tails, split-K wgrads over both images) against the ORACLE's autograd (lightning_module.py:242-244; train-mode
@@ -230,14 +229,19 @@ def test_c5_2048_bf16_vs_strict(model):
     assert rel_l2(b["pred_iou"], iou_s) <= 3e-2
 
 
-@pytest.mark.timeout(900)   # the oracle's fp32 2048^2 convs (MIOpen) can take minutes on a cold box
 def test_c5_one_image_strict_vs_oracle(model):
     from oracle import s3od_oracle as O
+    import time
     x, _ = _batch(1, 2048, 52)
     model.compute_dtype = "f32"
+    t0 = time.time()
     with torch.no_grad():
         out = model(x)
+        torch.cuda.synchronize()
+        t1 = time.time()
         ref = O.forward(x, _oracle_sd())
+        torch.cuda.synchronize()
+    print(f"C5 phases: engine f32 forward {t1 - t0:.1f} s, oracle forward {time.time() - t1:.1f} s", flush=True)
     e_m = rel_max(out["pred_masks"], ref["pred_masks"])
     e_i = rel_max(out["pred_iou"], ref["pred_iou"])
     print(f"C5 strict vs oracle @2048: logits {e_m:.3g}, iou {e_i:.3g}")
@@ -246,7 +250,6 @@ def test_c5_one_image_strict_vs_oracle(model):
 
 
 # ------------------------------------------------------------------------------------ bf16 vs the oracle
-@pytest.mark.timeout(900)   # the oracle's fp32 2048^2 convs (MIOpen) can take minutes on a cold box
 def test_bf16_vs_oracle_production_sizes(model):
     """The bf16 fast path checked against the ORACLE (not against the build's own f32 path) at the sizes the
     metric is quoted on: image 0 of a bs-8 1024^2 batch (C2) and of a bs-4 2048^2 batch (C5), and a bs-1

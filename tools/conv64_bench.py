@@ -2,7 +2,7 @@
 with the ReLU' mask and the bias column sums) at bs 16 x 1024^2: the register-weight kernel (default) vs the
 implicit GEMM (S3OD_CONV_RW=0, read per call), in one process, interleaved rounds; outputs compared (dev tool).
 
-    python tools/conv64_bench.py [B] [H]        (ARMS=RW_GB=0,RW_GB=4: other S3OD_ knobs as the arms)
+    python tools/conv64_bench.py [B] [H]        (ARMS=RW_GB=0,RW_GB=2: other S3OD_ knobs as the arms)
 """
 import os
 os.environ.setdefault("S3OD_AB", "1")   # knobs toggled per call (csrc/common.hpp S3OD_KNOB)
@@ -64,7 +64,7 @@ def main():
     def heads(lg, hs):
         lib()("s3od_mask_heads_fwd", BF16, B, H, W, 3, x, hw1, hb1, hw2, hb2, lg, hs, stream())
 
-    arms = os.environ.get("ARMS", "CONV_RW=0,CONV_RW=1").split(",")   # e.g. ARMS=RW_GB=0,RW_GB=2,RW_GB=4
+    arms = os.environ.get("ARMS", "CONV_RW=0,CONV_RW=1").split(",")   # e.g. ARMS=RW_GB=0,RW_GB=2
     for rnd in range(3):
         for rw in arms:
             kn, val = rw.split("=")
