@@ -20,7 +20,12 @@ build/attention.o: $(CSRC)/attention.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(FLAGS) $(ATTN_FLAGS) -c $< -o $@
 
-# the LDS-DMA 3x3 weight gradient keeps its MFMA accumulators in AGPRs (no VGPR form; see the file header)
+# the LDS-DMA 3x3 weight gradient and the 4-wave 256x256 GEMM keep their MFMA accumulators in AGPRs (no VGPR
+# form; see the file headers)
+build/gemm_q.o: $(CSRC)/gemm_q.hip $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(filter-out -mllvm -amdgpu-mfma-vgpr-form=1,$(FLAGS)) -c $< -o $@
+
 build/wgrad_dma.o: $(CSRC)/wgrad_dma.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(filter-out -mllvm -amdgpu-mfma-vgpr-form=1,$(FLAGS)) -c $< -o $@

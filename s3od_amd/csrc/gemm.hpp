@@ -1194,22 +1194,30 @@ __global__ void __launch_bounds__(GEMM_THREADS, 1) igemm_pp_kernel(LA la0, LB lb
       __builtin_amdgcn_s_setprio(0);
       raw_barrier();
     };
+    // DMA issue spread over the four load segments (round 5 issued both B halves in phase 0 and both A halves in
+    // phase 3, making those load segments outlast the partner's 16 MFMAs): B half 0 / 1 of tile t+1 in phases 0 / 1
+    // (their buffer's last reads were in tile t-1); A half 0 of tile t+2 in phase 2 -- read only by the wr = 0 waves,
+    // whose last reads (phase 1) every wave has waited for before the barrier that opens its phase 2; A half 1 in
+    // phase 3 -- read by the wr = 1 waves, which wait for their phase-1 reads one barrier later, still before any
+    // wave's phase 3.
     for (int t = 0; t < nt; ++t) {
       char* cb = smem + (t & 1) * STG;
       char* nb = smem + ((t + 1) & 1) * STG;
       const char* As = cb + wr * HB;
       const char* Bs = cb + (2 + (wc >> 1)) * HB + boff;
-      // phase 0: quadrant (0,0); B halves of tile t+1
+      // phase 0: quadrant (0,0); B half 0 of tile t+1
       rdA(As, 0); rdB(Bs, 0);
-      if (t + 1 < nt) { lb0.issue(kt0 + t + 1, nb + 2 * HB); lb1.issue(kt0 + t + 1, nb + 3 * HB); }
+      if (t + 1 < nt) lb0.issue(kt0 + t + 1, nb + 2 * HB);
       mm(0, 0);
-      // phase 1: quadrant (0,1); the tile's last LDS reads
+      // phase 1: quadrant (0,1); the tile's last LDS reads; B half 1 of tile t+1
       rdB(Bs, 1); rdA(As, 1);
+      if (t + 1 < nt) lb1.issue(kt0 + t + 1, nb + 3 * HB);
       mm(0, 1);
-      // phase 2: quadrant (1,1)
+      // phase 2: quadrant (1,1); A half 0 of tile t+2 into this tile's buffer
+      if (t + 2 < nt) la0.issue(kt0 + t + 2, cb);
       mm(1, 1);
-      // phase 3: quadrant (1,0); A halves of tile t+2 into this tile's buffer; retire tile t+1
-      if (t + 2 < nt) { la0.issue(kt0 + t + 2, cb); la1.issue(kt0 + t + 2, cb + HB); wait_vmcnt<NA>(); }
+      // phase 3: quadrant (1,0); A half 1 of tile t+2; retire tile t+1 (A issued in tile t-1, B in phases 0 / 1)
+      if (t + 2 < nt) { la1.issue(kt0 + t + 2, cb + HB); wait_vmcnt<NA>(); }
       else if (t + 1 < nt) wait_vmcnt<0>();
       mm(1, 0);
     }
@@ -1234,10 +1242,18 @@ __global__ void __launch_bounds__(GEMM_THREADS, 1) igemm_pp_kernel(LA la0, LB lb
 }
 constexpr int PP_LDS = 128 * (256 + 4) * 4;   // C chunk (133 KB) >= the two 64 KB K stages
 
-// WM_: waves along M (0 = by tile shape); e.g. 512x64 tiles use WM_=8 for 64x64 per-wave tiles
+// the 4-wave 256x256 kernel (gemm_q.hip, its own translation unit: AGPR accumulators); instantiated there for the
+// linears' (loader, epilogue) combinations
+template <class LA, class LB, class EPI>
+int launch_igemm_q(LA la, LB lb, EPI epi, int M, int N, int KTILES, int split, int zdim_extra, hipStream_t st);
+
+// WM_: waves along M (0 = by tile shape); e.g. 512x64 tiles use WM_=8 for 64x64 per-wave tiles; WM_ = -1: gemm_q.hip
 template <typename T, int BM, int BN, class LA, class LB, class EPI, int NST = 3, int WM_ = 0>
 static int launch_igemm(LA la, LB lb, EPI epi, int M, int N, int KTILES, int split, int zdim_extra, hipStream_t st) {
-  if constexpr (LA::ROWS * 2 == BM) {           // half-row loaders: the 256x256 ping-pong kernel
+  if constexpr (WM_ < 0) {
+    static_assert(BM == 256 && BN == 256 && sizeof(T) == 2, "q config");
+    return launch_igemm_q(la, lb, epi, M, N, KTILES, split, zdim_extra, st);
+  } else if constexpr (LA::ROWS * 2 == BM) {    // half-row loaders: the 256x256 ping-pong kernel
     static_assert(BM == 256 && BN == 256 && LB::ROWS == 128 && sizeof(T) == 2, "ping-pong config");
     if (!la.buf_ok() || !lb.buf_ok()) {
       s3od_set_error("igemm: operand window too large for a buffer descriptor or gather channels < %d", KT<T>::BK / 2);

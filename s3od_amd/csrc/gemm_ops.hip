@@ -24,6 +24,7 @@ static int gemm_cfg() { return S3OD_KNOB("S3OD_GEMM_CFG", -1); }
 template <int BM_, int BN_, int NST_, int W_ = GEMM_WAVES, int WM_ = 0, bool PP_ = false> struct TileCfg {
   static constexpr int BM = BM_, BN = BN_, NST = NST_, W = W_, WM = WM_;
   static constexpr bool PP = PP_;
+  static constexpr bool SLAB = PP_ || WM_ < 0;   // split-K partials into caller slabs (the 256x256 kernels)
   static constexpr int LM = PP_ ? BM_ / 2 : BM_, LN = PP_ ? BN_ / 2 : BN_;
 };
 // a conv whose output-channel tile is narrower than 256 cannot run the ping-pong kernel
@@ -50,9 +51,13 @@ static bool pp_pays(int M, int N) {
   const long tiles = (long)(M / 256) * cdiv(N, 256), rounds = (tiles + 255) / 256;
   return tiles >= 256 && (double)tiles / (double)(rounds * 256) >= 0.95;
 }
-template <typename T, class F> static int with_cfg(int def, F f) {
+// Q: the op may run config 6, the 4-wave 256x256 kernel (gemm_q.hip: instantiated for the linears only)
+template <typename T, bool Q = false, class F> static int with_cfg(int def, F f) {
   int c = tl_cfg >= 0 ? tl_cfg : gemm_cfg(); if (c < 0) c = def;
   switch (c) {
+    case 6:
+      if constexpr (Q && sizeof(T) == 2) return f(TileCfg<256, 256, 2, 4, -1>{});
+      else return f(TileCfg<128, 128, 2>{});
     case 1: return f(TileCfg<128, 128, 2>{});
     case 2: return f(TileCfg<128, 128, 3>{});
     case 3: return f(TileCfg<256, 128, 2>{});
@@ -1441,7 +1446,7 @@ int s3od_linear_fwd(int dtype, int M, int N, int K, const void* x, long ldx, con
       // (plain bias-only epilogues stay on 128x128: the DPT projections M=65536 N=1024 K=768 157 -> 146 us)
       const int def = (pp_pays(M, N) && N % 256 == 0 && (res1 || act == ACT_GELU || act == ACT_GELU_SG || K >= 2048)) ? 5
                       : (K >= 2048 ? 0 : 1);
-      return with_cfg<T>(def, [&](auto C) -> int {
+      return with_cfg<T, true>(def, [&](auto C) -> int {
         constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
         DenseKC<T, decltype(C)::LM, decltype(C)::W> la{(const T*)x, ldx, M, K, 0};
         DenseKC<T, decltype(C)::LN, decltype(C)::W> lb{(const T*)w, (long)K, N, K, 0};
@@ -1483,7 +1488,7 @@ int s3od_linear_dgrad(int dtype, int M, int N, int K, const void* dy, long lddy,
     const int KTILES = cdiv(K, KT<T>::BK);
     // ping-pong 256x256 for the long-K dgrads (up 441 -> 374 us, qkv 334 -> 292); 128x128 for K = 768
     const int def = (pp_pays(M, N) && K >= 2048 && N % 256 == 0) ? 5 : 1;
-    return with_cfg<T>(def, [&](auto C) -> int {
+    return with_cfg<T, true>(def, [&](auto C) -> int {
       constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
       DenseKC<T, decltype(C)::LM, decltype(C)::W> la{(const T*)dy, lddy, M, K, 0};
       DenseMC<T, decltype(C)::LN, decltype(C)::W> lb{(const T*)w, (long)N, K, N};
@@ -1515,8 +1520,8 @@ static long linear_wgrad_slab_floats(int dtype, int Nout, int Kin, int rows, int
   if (dtype != S3OD_BF16 || !slab_ok() || Kin % 4 != 0) return 0;
   const int KTILES = cdiv(rows, KT<bf16>::BK);
   const int def = linear_wgrad_def_cfg(Nout, Kin, rows);
-  return with_cfg<bf16>(def, [&](auto C) -> long {
-    if constexpr (!decltype(C)::PP) return 0;
+  return with_cfg<bf16, true>(def, [&](auto C) -> long {
+    if constexpr (!decltype(C)::SLAB) return 0;
     else {
       const int sp = split > 0 ? split : wgrad_split<bf16, 256, 256, 2>(cdiv(Nout, 256) * cdiv(Kin, 256), KTILES);
       return sp > 1 ? (long)sp * Nout * Kin : 0;
@@ -1542,12 +1547,12 @@ int s3od_linear_wgrad(int dtype, int Nout, int Kin, int rows, const void* dy, lo
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(rows, KT<T>::BK);
     const int def = linear_wgrad_def_cfg(Nout, Kin, rows);
-    return with_cfg<T>(def, [&](auto C) -> int {
+    return with_cfg<T, true>(def, [&](auto C) -> int {
       constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
       int sp = split > 0 ? split : wgrad_split<T, BM, BN, NST>(cdiv(Nout, BM) * cdiv(Kin, BN), KTILES);
       DenseMC<T, decltype(C)::LM, decltype(C)::W> la{(const T*)dy, lddy, rows, Nout};
       DenseMC<T, decltype(C)::LN, decltype(C)::W> lb{(const T*)x, ldx, rows, Kin};
-      if constexpr (decltype(C)::PP) {
+      if constexpr (decltype(C)::SLAB) {
         if (slab) {
           EpiWgradPart e{slab, Nout, Kin};
           int rc = launch_igemm<T, BM, BN, decltype(la), decltype(lb), decltype(e), NST, decltype(C)::WM>(la, lb, e, Nout, Kin, KTILES, sp, 1, st);
