@@ -128,6 +128,11 @@ static inline bool s3od_ab_mode() {
 // counted wait on this wave's vector-memory queue (LDS-DMA pieces, loads and stores count together, in issue order)
 template <int N> DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 DEV void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// vmcnt(0) through the builtin (lgkmcnt 15, expcnt 7 = no wait there): the waitcnt pass cannot see the inline-asm waits
+// above, so after an LDS-DMA main loop it still counts those DMAs as in flight and puts a vmcnt(0) in front of EVERY
+// later LDS read -- in an epilogue, behind the previous segment's global stores (vmcnt counts stores too), which
+// serialises the stores.  One of these after the main loop clears its scoreboard.
+DEV void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 // s_barrier WITHOUT the vmcnt(0) a __syncthreads() emits: LDS-DMA stays in flight across it
 DEV void raw_barrier() { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); }
 DEV void lds_barrier() { wait_lgkm0(); __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); }

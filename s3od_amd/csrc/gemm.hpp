@@ -799,6 +799,7 @@ __global__ void __launch_bounds__(GEMM_THREADS) igemm_kernel(LA la, LB lb, EPI e
       cur = nxt;
     }
   }
+  vm_drain();
   lds_barrier();
   // stage the C tile to LDS (fp32) in row chunks of CROWS and hand each chunk to the epilogue
   float* ct = (float*)smem;
@@ -875,7 +876,7 @@ enum { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_GELU_BWD = 3, ACT_RELU_BWD 
 // ACT_RELU_BWD: o = v * (res1 > 0)    (res1 = saved activation output, not added)
 // ACT_GELU_SG:  o = gelu(v) and `pre` receives gelu'(v) instead of the pre-activation (one erf serves both)
 // ACT_MUL:      o = v * res1          (res1 = the saved gelu'(v) of ACT_GELU_SG, not added)
-template <typename TO, typename TR, typename TP = TO> struct EpiStd {
+template <typename TO, typename TR, typename TP = TO, int EB = 4> struct EpiStd {
   // pre = acc + bias[n] ;  v = pre*scale[n] + shift[n] ;  out = act(v) (+res1 +res2)
   TO* out; long ldo; int coff;          // output row stride / channel offset
   const float* bias; const float* scale; const float* shift;
@@ -903,59 +904,27 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
       }
     }
     const bool fixed_cols = NT % (BN / 8) == 0;
-    // residual rows of a thread with <= 4 segments are all loaded before its first store: inside the
-    // segment loop each load would come after the previous segment's stores, and its wait (vmcnt is
-    // in issue order) would drain them.  Rows outside the output load row 0 (address select, not a
-    // branch around the load).  Larger tiles (the ping-pong kernel's 8 segments) keep the loop form:
-    // 8 prefetched rows beside its live accumulators spill.  bf16 residuals only (the GELU'/ReLU'
-    // pre-activations of dgrad, 587 vs 617 us for down-dgrad N3072 K768); the f32 residual-stream
-    // adds of o_proj/down fwd measured 1-2% slower with their 32 B rows held.
-    constexpr int PF = 4;
-    const int spr_ = BN / 8, rpi_ = NT / spr_;
-    const bool pf = sizeof(TR) == 2 && (res1 != nullptr) && fixed_cols && BM % rpi_ == 0 && BM / rpi_ <= PF;
-    Row8<TR> pr1[PF];
-    if (pf) {
-      const int r0 = tid / spr_, nn = n0 + (tid % spr_) * 8;
-#pragma unroll
-      for (int it = 0; it < PF; it++) {
-        const int m = m0 + r0 + it * rpi_;
-        const long o = (it < BM / rpi_ && m < M && nn < N) ? rm.map(m) : -1;
-        pr1[it].load(res1 + (o >= 0 ? o : 0) * ldr1 + (nn < N ? nn : 0));
-      }
-    }
-    for_segments(ct, LDT, BM, BN, m0, n0, M, N, tid, NT, [&](int m, int n, const float* a, int r, int) {
+    // one segment: 8 columns of row m (orow = its output row), a = the 8 staged accumulators, r1 = the 8 res1 values
+    // (read only when res1 is set: an array, never a pointer select, which would keep it in scratch).  ACT is a
+    // compile-time constant: the activation is dispatched once, outside the loops.
+    auto seg = [&](auto ACTC, long orow, int n, const float (&a)[8], const float (&r1)[8], const float (&bb)[8],
+                   const float (&ss)[8], const float (&hh)[8]) {
+      constexpr int A = decltype(ACTC)::value;
       float pv[8], v[8], o[8];
-      const long orow = rm.map(m);
-      if (fixed_cols) {
 #pragma unroll
-        for (int e = 0; e < 8; e++) { pv[e] = a[e] + b8[e]; v[e] = pv[e] * s8[e] + h8[e]; }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; e++) { pv[e] = a[e] + (bias ? bias[n + e] : 0.f); v[e] = pv[e] * (scale ? scale[n + e] : 1.f) + (shift ? shift[n + e] : 0.f); }
-      }
-      if (pre && act != ACT_GELU_SG) store8<TP>(pre + orow * ldp + n, pv);
-      // act is uniform: branch once per segment, so the erf path is never speculated for the others
+      for (int e = 0; e < 8; e++) { pv[e] = a[e] + bb[e]; v[e] = pv[e] * ss[e] + hh[e]; }
+      if (A != ACT_GELU_SG && pre) store8<TP>(pre + orow * ldp + n, pv);
       constexpr bool FAST = sizeof(TP) == 2;     // bf16 compute: branch-free GELU (common.hpp)
-      float rp[8];
-      if (pf) {
-        const int it = (r - tid / spr_) / rpi_;            // compile-time after for_segments unrolls
+      if constexpr (A == ACT_GELU_BWD) {
 #pragma unroll
-        for (int q = 0; q < PF; q++)
-          if (q == it) pr1[q].get(rp);
-      }
-      if (act == ACT_GELU_BWD) {
-        float r[8]; if (pf) { for (int e = 0; e < 8; e++) r[e] = rp[e]; } else load8<TR>(res1 + orow * ldr1 + n, r);
+        for (int e = 0; e < 8; e++) o[e] = v[e] * (FAST ? gelu_fast_grad(r1[e]) : gelu_erf_grad(r1[e]));
+      } else if constexpr (A == ACT_RELU_BWD) {
 #pragma unroll
-        for (int e = 0; e < 8; e++) o[e] = v[e] * (FAST ? gelu_fast_grad(r[e]) : gelu_erf_grad(r[e]));
-      } else if (act == ACT_RELU_BWD) {
-        float r[8]; if (pf) { for (int e = 0; e < 8; e++) r[e] = rp[e]; } else load8<TR>(res1 + orow * ldr1 + n, r);
+        for (int e = 0; e < 8; e++) o[e] = r1[e] > 0.f ? v[e] : 0.f;
+      } else if constexpr (A == ACT_MUL) {
 #pragma unroll
-        for (int e = 0; e < 8; e++) o[e] = r[e] > 0.f ? v[e] : 0.f;
-      } else if (act == ACT_MUL) {
-        float r[8]; if (pf) { for (int e = 0; e < 8; e++) r[e] = rp[e]; } else load8<TR>(res1 + orow * ldr1 + n, r);
-#pragma unroll
-        for (int e = 0; e < 8; e++) o[e] = v[e] * r[e];
-      } else if (act == ACT_GELU_SG) {
+        for (int e = 0; e < 8; e++) o[e] = v[e] * r1[e];
+      } else if constexpr (A == ACT_GELU_SG) {
         float gd[8];
 #pragma unroll
         for (int e = 0; e < 8; e++) {
@@ -966,19 +935,12 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
         }
         if (pre) store8<TP>(pre + orow * ldp + n, gd);
       } else {
-        if (act == ACT_GELU) {
 #pragma unroll
-          for (int e = 0; e < 8; e++) o[e] = FAST ? gelu_fast(v[e]) : gelu_erf(v[e]);
-        } else if (act == ACT_RELU) {
+        for (int e = 0; e < 8; e++) o[e] = A == ACT_GELU ? (FAST ? gelu_fast(v[e]) : gelu_erf(v[e])) : A == ACT_RELU ? fmaxf(v[e], 0.f) : v[e];
+        if (res1) {
 #pragma unroll
-          for (int e = 0; e < 8; e++) o[e] = fmaxf(v[e], 0.f);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; e++) o[e] = v[e];
+          for (int e = 0; e < 8; e++) o[e] += r1[e];
         }
-        if (res1) { float r[8]; if (pf) { for (int e = 0; e < 8; e++) r[e] = rp[e]; } else load8<TR>(res1 + orow * ldr1 + n, r);
-#pragma unroll
-          for (int e = 0; e < 8; e++) o[e] += r[e]; }
       }
       if (res2) { float r[8]; load8<TR>(res2 + orow * ldr2 + n, r);
 #pragma unroll
@@ -988,7 +950,73 @@ template <typename TO, typename TR, typename TP = TO> struct EpiStd {
 #pragma unroll
         for (int e = 0; e < 8; e++) cs8[e] += o[e];
       }
-    });
+    };
+    auto dispatch = [&](auto body) {
+      switch (act) {
+        case ACT_RELU: body(std::integral_constant<int, ACT_RELU>{}); break;
+        case ACT_GELU: body(std::integral_constant<int, ACT_GELU>{}); break;
+        case ACT_GELU_BWD: body(std::integral_constant<int, ACT_GELU_BWD>{}); break;
+        case ACT_RELU_BWD: body(std::integral_constant<int, ACT_RELU_BWD>{}); break;
+        case ACT_GELU_SG: body(std::integral_constant<int, ACT_GELU_SG>{}); break;
+        case ACT_MUL: body(std::integral_constant<int, ACT_MUL>{}); break;
+        default: body(std::integral_constant<int, ACT_NONE>{}); break;
+      }
+    };
+    const int spr_ = BN / 8;
+    if (fixed_cols && BM % (NT / spr_) == 0) {
+      // a thread's segments are rows r0 + it * rpi of one 8-column group.  They run in batches of EB: the batch's
+      // staged accumulators (LDS) and res1 rows (global) are all read before its first store -- with a read per
+      // segment, each LDS read latency is exposed in turn and each residual load waits (vmcnt, in issue order)
+      // for every earlier segment's stores.  Rows outside the output read row 0 (address select, no branch).
+      const int rpi = NT / spr_, cs = tid % spr_, r0 = tid / spr_, n = n0 + cs * 8, nit = BM / rpi;
+      if (n < N) {
+        dispatch([&](auto ACTC) {
+#pragma unroll
+          for (int it0 = 0; it0 < nit; it0 += EB) {
+            __builtin_amdgcn_sched_barrier(0);     // no batch's reads hoisted above the previous batch (VGPRs)
+            float av[EB][8];
+            Row8<TR> q[EB];
+            long orow[EB];
+#pragma unroll
+            for (int u = 0; u < EB; u++) {
+              const int it = it0 + u, r = r0 + it * rpi, m = m0 + r;
+              if (it < nit) {
+                const float4* src = (const float4*)(ct + r * LDT + cs * 8);
+                const float4 x0 = src[0], x1 = src[1];
+                av[u][0] = x0.x; av[u][1] = x0.y; av[u][2] = x0.z; av[u][3] = x0.w;
+                av[u][4] = x1.x; av[u][5] = x1.y; av[u][6] = x1.z; av[u][7] = x1.w;
+                orow[u] = m < M ? rm.map(m) : 0;
+                if (res1) q[u].load(res1 + orow[u] * ldr1 + n);
+              }
+            }
+#pragma unroll
+            for (int u = 0; u < EB; u++) {
+              const int it = it0 + u;
+              if (it < nit && m0 + r0 + it * rpi < M) {
+                float r1v[8];
+                q[u].get(r1v);                     // unused (never read) without res1
+                seg(ACTC, orow[u], n, av[u], r1v, b8, s8, h8);
+              }
+            }
+          }
+        });
+      }
+    } else {
+      dispatch([&](auto ACTC) {
+        for_segments(ct, LDT, BM, BN, m0, n0, M, N, tid, NT, [&](int m, int n, const float* a, int, int) {
+          float av[8], bb[8], ss[8], hh[8], r1v[8];
+#pragma unroll
+          for (int e = 0; e < 8; e++) {
+            av[e] = a[e];
+            bb[e] = bias ? bias[n + e] : 0.f; ss[e] = scale ? scale[n + e] : 1.f; hh[e] = shift ? shift[n + e] : 0.f;
+            r1v[e] = 0.f;
+          }
+          const long orow = rm.map(m);
+          if (res1) load8<TR>(res1 + orow * ldr1 + n, r1v);
+          seg(ACTC, orow, n, av, r1v, bb, ss, hh);
+        });
+      });
+    }
     if (stats) {
       // column statistics of pre over this tile's valid rows: thread -> (col, row phase).  The fp64 atomics of
       // every tile of the grid would all land on the same 2N words; they are spread over S3OD_NREP replicas
@@ -1119,6 +1147,31 @@ template <> struct PPFrag<false> {
 // The epilogue stages C through the K-stage LDS in two 128-row chunks with LDS barriers only (a
 // __syncthreads() would drain the stores).  (A persistent variant -- the next tile's first K
 // stage issued behind this tile's stores -- measured within 5 % of this at 20 spilled VGPRs.)
+// Dev timeline build (-DS3OD_TIMELINE, tools/pp_timeline.py; never in the production library): the ping-pong kernel
+// records per block [start, main loop done, epilogue done, HW_ID / XCC_ID, C half 0 staged, half 0 done, half 1
+// staged, -] (s_memrealtime, 100 MHz) into s3od_tl[linear block][8], set per translation unit by s3od_dbg_timeline()
+#ifdef S3OD_TIMELINE
+static __device__ unsigned long long* s3od_tl;
+#define S3OD_TL(slot, v) do { if (s3od_tl && threadIdx.x == 0) s3od_tl[((long)blockIdx.z * gridDim.y * gridDim.x + \
+    blockIdx.y * gridDim.x + blockIdx.x) * 8 + (slot)] = (v); } while (0)
+#else
+#define S3OD_TL(slot, v) do { } while (0)
+#endif
+
+// block -> (M tile, N tile) of a 2-D grid: an XCD-contiguous linear index W (the blocks one XCD receives get
+// consecutive W), then row-major -- or, with G > 0, in groups of G M-tiles walked column-major, so the ~32 blocks an
+// XCD runs at once cover a G x (32 / G) patch and share G A-panels and 32 / G B-panels in that XCD's L2 instead of one
+// A-panel and 32 B-panels
+DEV void tile_of_block(int G, int& mt, int& nt) {
+  const int nN = gridDim.x, nM = gridDim.y, nwg = nN * nM;
+  const int L = blockIdx.y * nN + blockIdx.x;
+  const int q = nwg >> 3, r = nwg & 7, xcd = L & 7, idx = L >> 3;
+  const int W = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  if (G <= 0) { mt = W / nN; nt = W % nN; return; }
+  const int per = G * nN, g = W / per, w = W - g * per, m_first = g * G, gs = min(nM - m_first, G);
+  mt = m_first + w % gs; nt = w / gs;
+}
+
 template <class LA, class LB, class EPI>
 __global__ void __launch_bounds__(GEMM_THREADS, 1) igemm_pp_kernel(LA la0, LB lb0, EPI epi, int KTILES, int split, int flags) {
   typedef bf16 T;
@@ -1128,13 +1181,14 @@ __global__ void __launch_bounds__(GEMM_THREADS, 1) igemm_pp_kernel(LA la0, LB lb
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int wr = wave >> 2, wc = wave & 3;
+  S3OD_TL(0, __builtin_amdgcn_s_memrealtime());
+  S3OD_TL(3, ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32) |
+             (unsigned)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));
   int m0, n0;
   {
-    const int nwg = gridDim.x * gridDim.y;
-    const int L = blockIdx.y * gridDim.x + blockIdx.x;
-    const int q = nwg >> 3, r = nwg & 7, xcd = L & 7, idx = L >> 3;
-    const int W = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-    m0 = (W / gridDim.x) * BM; n0 = (W % gridDim.x) * BN;
+    int mt, nt_;
+    tile_of_block((flags >> 8) & 0xff, mt, nt_);
+    m0 = mt * BM; n0 = nt_ * BN;
   }
   const int per = (KTILES + split - 1) / split;
   const int kt0 = blockIdx.z * per, kt1 = min(KTILES, kt0 + per);
@@ -1223,24 +1277,57 @@ __global__ void __launch_bounds__(GEMM_THREADS, 1) igemm_pp_kernel(LA la0, LB lb
     }
     if (!wr && stag) raw_barrier();            // re-align the two halves
   }
-  float* ct = (float*)smem;
-#pragma unroll
-  for (int h = 0; h < 2; h++) {
+  S3OD_TL(1, __builtin_amdgcn_s_memrealtime());
+  vm_drain();
+  // The C tile goes through LDS (fp32) in two rounds of two 64-row quarters: round c stages rows [c*64, c*64+64) of
+  // each wave row half (wave row wr -> buffer wr), then the epilogue runs on both.  After round 0 every wave's first
+  // four accumulator row tiles are dead, so at most 64 accumulator VGPRs are live under the epilogue code (halves
+  // staged one at a time kept the wr = 1 waves' 128 live through half 0's epilogue).
+  float* ct0 = (float*)smem;
+  float* ct1 = ct0 + 64 * LDT;
+  // (a lambda on a compile-time round, not a loop: a loop this size stays rolled and indexes acc at run time,
+  // which puts all of acc on the stack)
+  auto round = [&](auto CC) {
+    constexpr int c = decltype(CC)::value;
     lds_barrier();
-    if (wr == h) {
+    {
+      float* dst = wr ? ct1 : ct0;
 #pragma unroll
-      for (int i = 0; i < 8; i++)
+      for (int i = 0; i < 4; i++)
 #pragma unroll
         for (int j = 0; j < 4; j++) {
           const int r = i * 16 + (lane & 15), col = wc * 64 + j * 16 + (lane >> 4) * 4;
-          *(f32x4*)(ct + r * LDT + col) = acc[i][j];
+          *(f32x4*)(dst + r * LDT + col) = acc[c * 4 + i][j];
         }
     }
     lds_barrier();
-    epi(ct, LDT, m0 + h * 128, n0, tid, 128, BN, GEMM_THREADS);
-  }
+    S3OD_TL(4 + 2 * c, __builtin_amdgcn_s_memrealtime());
+#ifdef S3OD_TIMELINE
+    // dev (timeline build, S3OD_PP_FLAGS bit 1): a bare bf16 store loop instead of the epilogue functor
+    if constexpr (std::is_same_v<EPI, EpiStd<bf16, bf16, bf16>>) {
+      if (flags & 2) {
+        const int cs = tid % 32, r0 = tid / 32;
+#pragma unroll
+        for (int it = 0; it < 8; it++) {
+          const int r = r0 + (it & 3) * 16;
+          const float* src_ = (it < 4 ? ct0 : ct1) + r * LDT + cs * 8;
+          const float4 a = ((const float4*)src_)[0], b = ((const float4*)src_)[1];
+          const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+          store8<bf16>(epi.out + (long)(m0 + (it < 4 ? 0 : 128) + c * 64 + r) * epi.ldo + n0 + cs * 8, v);
+        }
+        return;
+      }
+    }
+#endif
+    epi(ct0, LDT, m0 + c * 64, n0, tid, 64, BN, GEMM_THREADS);
+    epi(ct1, LDT, m0 + 128 + c * 64, n0, tid, 64, BN, GEMM_THREADS);
+    if (c == 0) S3OD_TL(5, __builtin_amdgcn_s_memrealtime());
+  };
+  round(std::integral_constant<int, 0>{});
+  round(std::integral_constant<int, 1>{});
+  S3OD_TL(2, __builtin_amdgcn_s_memrealtime());
 }
-constexpr int PP_LDS = 128 * (256 + 4) * 4;   // C chunk (133 KB) >= the two 64 KB K stages
+constexpr int PP_LDS = 128 * (256 + 4) * 4;   // two 64-row C quarters (133 KB) >= the two 64 KB K stages
 
 // the 4-wave 256x256 kernel (gemm_q.hip, its own translation unit: AGPR accumulators); instantiated there for the
 // linears' (loader, epilogue) combinations
@@ -1262,7 +1349,7 @@ static int launch_igemm(LA la, LB lb, EPI epi, int M, int N, int KTILES, int spl
     auto kfn = igemm_pp_kernel<LA, LB, EPI>;
     static const bool attr = ((void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS), true);   // once per process (thread-safe static init)
     (void)attr;
-    const int flags = S3OD_KNOB("S3OD_PP_FLAGS", 0);
+    const int flags = S3OD_KNOB("S3OD_PP_FLAGS", 0) | (S3OD_KNOB("S3OD_GEMM_GROUP", 0) & 0xff) << 8;
     dim3 grid(cdiv(N, BN), cdiv(M, BM), split * zdim_extra);
     hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), PP_LDS, st, la, lb, epi, KTILES, split, flags);
     return s3od_check_launch("igemm_pp");

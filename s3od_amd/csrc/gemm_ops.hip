@@ -1411,6 +1411,13 @@ __global__ void wgrad_permute_add_kernel(float* __restrict__ ws, float* __restri
 
 extern "C" {
 
+#ifdef S3OD_TIMELINE
+// dev timeline build only (tools/pp_timeline.py): where the ping-pong kernels of this file record their blocks
+int s3od_dbg_timeline(unsigned long long* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(s3od_tl), &buf, sizeof(buf)) == hipSuccess ? 0 : 1;
+}
+#endif
+
 // ---------------------------------------------------------------------------------- linear
 // pre = sum_k x[m,k] w[n,k] + bias[n];  out[rm(m), n] = act(pre*scale[n] + shift[n]) (+res1 +res2)
 // x: [M,K] (ld ldx) dtype T, w: [N,K] T, res: T or f32 (res_f32), out T or f32 (out_f32).

@@ -29,7 +29,7 @@ static_assert(Q_LDS <= 160 * 1024, "q kernel LDS budget");
 DEV void q_wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
 
 template <class LA, class LB, class EPI>
-__global__ void __launch_bounds__(Q_THREADS, 1) igemm_q_kernel(LA la, LB lb, EPI epi, int KTILES, int split) {
+__global__ void __launch_bounds__(Q_THREADS, 1) igemm_q_kernel(LA la, LB lb, EPI epi, int KTILES, int split, int group) {
   typedef bf16 T;
   static_assert(LA::ROWS == 256 && LB::ROWS == 256 && LA::NIW == 8 && LB::NIW == 8, "q kernel: 256-row loaders on 4 waves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -37,11 +37,9 @@ __global__ void __launch_bounds__(Q_THREADS, 1) igemm_q_kernel(LA la, LB lb, EPI
   const int wm = wave >> 1, wn = wave & 1;
   int m0, n0;
   {
-    const int nwg = gridDim.x * gridDim.y;
-    const int L = blockIdx.y * gridDim.x + blockIdx.x;
-    const int q = nwg >> 3, r = nwg & 7, xcd = L & 7, idx = L >> 3;
-    const int W = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-    m0 = (W / gridDim.x) * Q_BM; n0 = (W % gridDim.x) * Q_BN;
+    int mt, nt_;
+    tile_of_block(group, mt, nt_);
+    m0 = mt * Q_BM; n0 = nt_ * Q_BN;
   }
   const int per = (KTILES + split - 1) / split;
   const int kt0 = blockIdx.z * per, kt1 = min(KTILES, kt0 + per);
@@ -120,6 +118,7 @@ __global__ void __launch_bounds__(Q_THREADS, 1) igemm_q_kernel(LA la, LB lb, EPI
     mfmas(1);
   }
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // XDL write -> accumulator read (epilogue)
+  vm_drain();
   // stage the C tile (fp32) through LDS in two 128-row halves: waves wm = h write half h
   float* ct = (float*)smem;
 #pragma unroll
@@ -149,7 +148,8 @@ int launch_igemm_q(LA la, LB lb, EPI epi, int M, int N, int KTILES, int split, i
   static const bool attr = ((void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, Q_LDS), true);
   (void)attr;
   dim3 grid(cdiv(N, Q_BN), cdiv(M, Q_BM), split * zdim_extra);
-  hipLaunchKernelGGL(kfn, grid, dim3(Q_THREADS), Q_LDS, st, la, lb, epi, KTILES, split);
+  const int group = S3OD_KNOB("S3OD_GEMM_GROUP", 0);
+  hipLaunchKernelGGL(kfn, grid, dim3(Q_THREADS), Q_LDS, st, la, lb, epi, KTILES, split, group);
   return s3od_check_launch("igemm_q");
 }
 

@@ -23,11 +23,11 @@ TOOLS = [shutil.which("objcopy"), LLVM / "clang-offload-bundler", LLVM / "llvm-r
 # the counted-vmcnt kernels the product path launches: mangled-name prefixes (c++filt cannot demangle the __bf16
 # template arguments) or demangled-name patterns
 PRODUCTION = [
-    r"^_Z15igemm_pp_kernelI6Conv3AILi128ELb[01]ELi8EE7DenseKCIDF16bLi128ELi8EE6EpiStdIDF16bDF16bDF16bEE",
-    r"^_Z15igemm_pp_kernelI7DenseKCIDF16bLi128ELi8EE7DenseMCIDF16bLi128ELi8EE6EpiStdIDF16bDF16bDF16bEE",
+    r"^_Z15igemm_pp_kernelI6Conv3AILi128ELb[01]ELi8EE7DenseKCIDF16bLi128ELi8EE6EpiStdIDF16bDF16bDF16bLi4EEE",
+    r"^_Z15igemm_pp_kernelI7DenseKCIDF16bLi128ELi8EE7DenseMCIDF16bLi128ELi8EE6EpiStdIDF16bDF16bDF16bLi4EEE",
     r"^_Z15igemm_pp_kernelI7DenseKCIDF16bLi128ELi8EES1_6EpiQKVIDF16bEE",
-    r"^_Z15igemm_pp_kernelI7DenseKCIDF16bLi128ELi8EES1_6EpiStdIDF16bDF16bDF16bEE",
-    r"^_Z15igemm_pp_kernelI7DenseKCIDF16bLi128ELi8EES1_6EpiStdIffDF16bEE",
+    r"^_Z15igemm_pp_kernelI7DenseKCIDF16bLi128ELi8EES1_6EpiStdIDF16bDF16bDF16bLi4EEE",
+    r"^_Z15igemm_pp_kernelI7DenseKCIDF16bLi128ELi8EES1_6EpiStdIffDF16bLi4EEE",
     r"^_Z15igemm_pp_kernelI7DenseMCIDF16bLi128ELi8EES1_12EpiWgradPartE",
     r"^_Z12igemm_kernelIDF16bLi128ELi128ELi2E",
     r"^_Z12igemm_kernelIDF16bLi256ELi128ELi3E",
