@@ -1449,10 +1449,9 @@ int s3od_linear_fwd(int dtype, int M, int N, int K, const void* x, long ldx, con
       typedef decltype(tout) TO; typedef decltype(tres) TR;
       // measured (tools/lin_sweep.py, bs 16 1024^2): the 256x256 ping-pong kernel for the large ViT
       // linears (o_proj 241 -> 215 us, up 576 -> 563, down 487 -> 418); else 256x128 x 3 stages for
-      // K >= 2048, 128x128 otherwise
-      // (plain bias-only epilogues stay on 128x128: the DPT projections M=65536 N=1024 K=768 157 -> 146 us)
-      const int def = (pp_pays(M, N) && N % 256 == 0 && (res1 || act == ACT_GELU || act == ACT_GELU_SG || K >= 2048)) ? 5
-                      : (K >= 2048 ? 0 : 1);
+      // K >= 2048, 128x128 otherwise.  Since the quarter-staged ping-pong epilogue (round 6) the plain bias-only
+      // DPT projections M=65536 K=768 run on it too (tools/lib_ab.py: N 1024 160 -> 156 us, 512 90 -> 87, 256 54 -> 52)
+      const int def = (pp_pays(M, N) && N % 256 == 0) ? 5 : (K >= 2048 ? 0 : 1);
       return with_cfg<T, true>(def, [&](auto C) -> int {
         constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
         DenseKC<T, decltype(C)::LM, decltype(C)::W> la{(const T*)x, ldx, M, K, 0};
@@ -1493,8 +1492,10 @@ int s3od_linear_dgrad(int dtype, int M, int N, int K, const void* dy, long lddy,
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     const int KTILES = cdiv(K, KT<T>::BK);
-    // ping-pong 256x256 for the long-K dgrads (up 441 -> 374 us, qkv 334 -> 292); 128x128 for K = 768
-    const int def = (pp_pays(M, N) && K >= 2048 && N % 256 == 0) ? 5 : 1;
+    // ping-pong 256x256 for the long-K dgrads (up 441 -> 374 us, qkv 334 -> 292) and the K = 768 ones with an
+    // activation-derivative epilogue (down-projection x gelu': 519 -> 500 us, round 6); 128x128 for plain K = 768
+    // (o_proj 118 vs 118 us)
+    const int def = (pp_pays(M, N) && N % 256 == 0 && (K >= 2048 || act != ACT_NONE)) ? 5 : 1;
     return with_cfg<T, true>(def, [&](auto C) -> int {
       constexpr int BM = decltype(C)::BM, BN = decltype(C)::BN, NST = decltype(C)::NST;
       DenseKC<T, decltype(C)::LM, decltype(C)::W> la{(const T*)dy, lddy, M, K, 0};

@@ -115,18 +115,18 @@ def lin(libs, rounds):
         q, k, v = (torch.empty(B * 12, Nt, 64, device="cuda", dtype=torch.bfloat16) for _ in range(3))
         return (lambda: L("s3od_qkv_rope_fwd", BF16, B, Nt, P, 12, x768, wq, bq, cs, sn, q, k, v, st)), q
 
-    def c_fwd(w, b, N, K, x, act=0, resf=False, scale=None):
+    def c_fwd(w, b, N, K, x, act=0, resf=False, scale=None, pre=True):
         def mk(L):
             out = torch.empty(M, N, device="cuda", dtype=torch.float32 if resf else torch.bfloat16)
-            pr = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            pr = torch.empty(M, N, device="cuda", dtype=torch.bfloat16) if pre else None
             return (lambda: L("s3od_linear_fwd", BF16, M, N, K, x, K, w, b, scale, None, act, res if resf else None, N, None, 0,
                               int(resf), out, N, int(resf), pr, N, 0, 0, 0, st)), out
         return mk
 
-    def c_dgrad(w, N, K, dy):
+    def c_dgrad(w, N, K, dy, act=0, aux=None):
         def mk(L):
             out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-            return (lambda: L("s3od_linear_dgrad", BF16, M, N, K, dy, K, w, 0, None, N, out, N, 0, 0, 0, 0, None, st)), out
+            return (lambda: L("s3od_linear_dgrad", BF16, M, N, K, dy, K, w, act, aux, N, out, N, 0, 0, 0, 0, None, st)), out
         return mk
 
     def c_wgrad(Nout, Kin, dy, x):
@@ -146,6 +146,11 @@ def lin(libs, rounds):
              ("down fwd N768 K3072 res f32", 2.0 * M * D * F, c_fwd(wd, bd, D, F, x3072, resf=True, scale=sd)),
              ("up dgrad N768 K3072", 2.0 * M * D * F, c_dgrad(wu, D, F, dy3072)),
              ("qkv dgrad N768 K2304", 2.0 * M * D * 3 * D, c_dgrad(wq, D, 3 * D, r(M, 3 * D))),
+             ("down dgrad N3072 K768 x gelu'", 2.0 * M * D * F, c_dgrad(wd, F, D, dy768, act=6, aux=r(M, F))),
+             ("o_proj dgrad N768 K768", 2.0 * M * D * D, c_dgrad(wo, D, D, dy768)),
+             ("DPT proj fwd N1024 K768 bias", 2.0 * M * 1024 * D, c_fwd(r(1024, D), r(1024, dt=torch.float32), 1024, D, x768, pre=False)),
+             ("DPT proj fwd N512 K768 bias", 2.0 * M * 512 * D, c_fwd(r(512, D), r(512, dt=torch.float32), 512, D, x768, pre=False)),
+             ("DPT proj fwd N256 K768 bias", 2.0 * M * 256 * D, c_fwd(r(256, D), r(256, dt=torch.float32), 256, D, x768, pre=False)),
              ("wgrad 3072x768", 2.0 * M * F * D, c_wgrad(F, D, dy3072, x768)),
              ("wgrad 768x3072", 2.0 * M * D * F, c_wgrad(D, F, dy768, x3072)),
              ("conv fwd 256->256 3x3 @256^2 bs16", 2.0 * 16 * 256 * 256 * 256 * 256 * 9, c_conv)]
