@@ -1248,10 +1248,17 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int sp, int M,
   const long i4 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   const long MN = (long)M * N;
   if (i4 >= MN) return;
+  // the slabs' loads go out 8 at a time before any add (a load-add chain waits out one memory latency per slab:
+  // 81 us for 7 slabs of 3072 x 768 in the step, 4x the bytes' HBM time); summation order z = 0, 1, .. unchanged
   float4 s = *(const float4*)(ws + i4);
-  for (int z = 1; z < sp; z++) {
-    const float4 v = *(const float4*)(ws + (long)z * MN + i4);
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  for (int z0 = 1; z0 < sp; z0 += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (z0 + u < sp) v[u] = *(const float4*)(ws + (long)(z0 + u) * MN + i4);
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (z0 + u < sp) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
   }
   const int m = (int)(i4 / N), n = (int)(i4 - (long)m * N);
   if (taps == 1) {

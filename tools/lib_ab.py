@@ -130,9 +130,14 @@ def lin(libs, rounds):
         return mk
 
     def c_wgrad(Nout, Kin, dy, x):
+        """with the caller-owned split-K slab the engine passes (s3od_linear_wgrad_ws): slab partials + reduce"""
         def mk(L):
             dw = torch.zeros(Nout, Kin, device="cuda")
-            return (lambda: (dw.zero_(), L("s3od_linear_wgrad", BF16, Nout, Kin, M, dy, Nout, x, Kin, dw, 0, None, 0, st))), dw
+            nb = ctypes.c_long(0)
+            L("s3od_linear_wgrad_ws", BF16, Nout, Kin, M, 0, ctypes.addressof(nb))
+            slab = torch.empty(max(nb.value, 4) // 4, device="cuda")
+            return (lambda: (dw.zero_(), L("s3od_linear_wgrad", BF16, Nout, Kin, M, dy, Nout, x, Kin, dw, 0, slab, nb.value,
+                                           st))), dw
         return mk
 
     def c_conv(L):
