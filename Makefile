@@ -35,13 +35,13 @@ build/%.o: $(CSRC)/%.hip $(HDRS)
 	$(HIPCC) $(FLAGS) -c $< -o $@
 
 s3od_amd/libs3od_hip.so: $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -lhipblaslt -o $@
 
 # dev: the ping-pong kernels of gemm_ops.hip with the block timeline compiled in (tools/pp_timeline.py)
 timeline: $(OBJS)
 	@mkdir -p build_tl tl_lib
 	$(HIPCC) $(FLAGS) -DS3OD_TIMELINE -c $(CSRC)/gemm_ops.hip -o build_tl/gemm_ops.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(filter-out build/gemm_ops.o,$(OBJS)) build_tl/gemm_ops.o -o tl_lib/libs3od_hip.so
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(filter-out build/gemm_ops.o,$(OBJS)) build_tl/gemm_ops.o -lhipblaslt -o tl_lib/libs3od_hip.so
 
 clean:
 	rm -rf build s3od_amd/libs3od_hip.so

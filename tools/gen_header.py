@@ -91,6 +91,8 @@ def collect():
         if i < 0:
             continue
         for m in SIG.finditer(txt, i):
+            if m.group(2).startswith("s3od_dbg_"):
+                continue                    # dev-build entry points (#ifdef S3OD_TIMELINE), not part of the ABI
             args = " ".join(m.group(3).split())
             out.append((m.group(2), m.group(1), args, f.name))
     return out
