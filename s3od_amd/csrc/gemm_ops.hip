@@ -1487,12 +1487,6 @@ int s3od_linear_dgrad(int dtype, int M, int N, int K, const void* dy, long lddy,
                       int act, const void* aux, long ldaux, void* dx, long lddx, int out_f32,
                       int row_mode, int P, int prefix, float* colsum, void* stream) {
   S3OD_REQUIRE(K % 8 == 0 && N % 8 == 0, "linear_dgrad: K,N %% 8");
-  // plain bf16 data gradients -- no activation derivative, no column sums, dense rows; aux an accumulate -- are plain
-  // library GEMMs: hipBLASLt (blaslt.hip), 1.24-1.35x faster on the ViT backward's long-K shapes.  S3OD_DGRAD_BLASLT=0
-  // (or no algorithm for the shape) keeps them on this file's kernels.
-  if (dtype == S3OD_BF16 && act == ACT_NONE && !out_f32 && row_mode == 0 && !colsum && S3OD_KNOB("S3OD_DGRAD_BLASLT", 1) &&
-      blaslt_gemm_rm(dy, lddy, w, N, aux, ldaux, dx, lddx, M, N, K, (hipStream_t)stream) == 0)
-    return s3od_check_launch("linear_dgrad (hipBLASLt)");
   if (row_mode == 0 && split_tail(M)) {
     const int M1 = M & ~255, M2 = M - M1;
     int rc = s3od_linear_dgrad(dtype, M1, N, K, dy, lddy, w, act, aux, ldaux, dx, lddx, out_f32, row_mode, P, prefix,
@@ -1504,6 +1498,15 @@ int s3od_linear_dgrad(int dtype, int M, int N, int K, const void* dy, long lddy,
                              aux ? (const char*)aux + M1 * ldaux * eo : nullptr, ldaux, (char*)dx + M1 * lddx * eo, lddx,
                              out_f32, row_mode, P, prefix, colsum, stream);
   }
+  // plain bf16 data gradients -- no activation derivative, no column sums, dense rows; aux an accumulate -- are plain
+  // library GEMMs: hipBLASLt (blaslt.hip), 1.24-1.35x faster on the ViT backward's long-K shapes.  Only the whole
+  // 256-row panels: left a tail, hipBLASLt adds a 16x16-tile kernel over the full K for it, which beside the side
+  // stream's weight gradients took 300-370 us in the step (profiles/r06z_summary.md) -- the M-tail stays on the skinny
+  // tail kernel above (TailCfg).  S3OD_DGRAD_BLASLT=0 (or no algorithm for the shape) keeps everything here.
+  if (tl_cfg != 1 && dtype == S3OD_BF16 && act == ACT_NONE && !out_f32 && row_mode == 0 && !colsum &&
+      S3OD_KNOB("S3OD_DGRAD_BLASLT", 1) &&
+      blaslt_gemm_rm(dy, lddy, w, N, aux, ldaux, dx, lddx, M, N, K, (hipStream_t)stream) == 0)
+    return s3od_check_launch("linear_dgrad (hipBLASLt)");
   RowMap rm = dense_rm(); rm.mode = row_mode; rm.P = P; rm.prefix = prefix;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
