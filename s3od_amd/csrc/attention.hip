@@ -116,12 +116,20 @@ DEV float xmax4(float v) { v = fmaxf(v, __shfl_xor(v, 16)); return fmaxf(v, __sh
 DEV float xsum4(float v) { v += __shfl_xor(v, 16); return v + __shfl_xor(v, 32); }
 }  // namespace
 
-template <typename T>
+// DMA (bf16): K / V tiles by LDS-DMA (buffer_load ... lds, 4 x 1 KiB pieces per wave and tile, the image swizzle
+// applied to each lane's source chunk) instead of buffer loads into registers + ds_write: no staging registers and no
+// LDS store instructions in the loop; the next tile's pieces land during the current tile (vmcnt(0) + the barrier)
+template <typename T, bool DMA = false>
 __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V,
                                                         T* __restrict__ O, float* __restrict__ LSE, int N, int H, int fast) {
   constexpr bool F32 = std::is_same<T, float>::value;
+  static_assert(!DMA || !F32, "attn_fwd: LDS-DMA staging is the bf16 path");
   typedef TileL<T> L;
-  __shared__ __attribute__((aligned(16))) char smem[4 * L::BYTES];
+  // DMA: the second K / V stage is its own array -- a distinct object, so alias analysis can tell this tile's LDS
+  // reads from the next tile's DMA without relying on offsets (with one array it waited vmcnt(0) before the V^T reads
+  // of every other tile)
+  __shared__ __attribute__((aligned(DMA ? 1024 : 16))) char smem[(DMA ? 2 : 4) * L::BYTES];
+  __shared__ __attribute__((aligned(DMA ? 1024 : 16))) char smem1[DMA ? 2 * L::BYTES : 16];
   const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
   const T* Qp = Q + (long)bh * N * 64;
@@ -163,6 +171,165 @@ __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(const T* __restrict__ 
   negm[0] = negm[1] = f32x4{0, 0, 0, 0};
   lacc[0] = lacc[1] = f32x4{0, 0, 0, 0};
 
+  if constexpr (DMA) {
+  const int nkt = (N + 63) / 64;
+  // the per-tile work on the staged K / V images ks, vs (both staging forms)
+  auto tile_compute = [&](int kt, const char* ks, const char* vs) {
+    // a wave whose 32 queries are all >= N (the partial last block: N = 4096 + 5 prefix tokens) only helps stage K / V
+    if (active) {
+    // ---- S^T = K Q^T (- m) : acc[kb][qs], element i: key = kb*16 + 4g + i, query = qs*16 + li
+    f32x4 s[4][2];
+#pragma unroll
+    for (int kb = 0; kb < 4; kb++) {
+      if constexpr (F32) {
+        s[kb][0] = f32x4{0, 0, 0, 0}; s[kb][1] = f32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int kk = 0; kk < QK; kk++) {
+          float a = *(const float*)(ks + L::krow(kb * 16 + li, (kk * 4 + g) * 4));
+          s[kb][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, qf[0][kk], s[kb][0], 0, 0, 0);
+          s[kb][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, qf[1][kk], s[kb][1], 0, 0, 0);
+        }
+      } else {
+        bf16x8 a0 = *(const bf16x8*)(ks + L::krow(kb * 16 + li, g * 16));
+        bf16x8 a1 = *(const bf16x8*)(ks + L::krow(kb * 16 + li, 64 + g * 16));
+        s[kb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, qf[0][0], negm[0], 0, 0, 0);
+        s[kb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, qf[1][0], negm[1], 0, 0, 0);
+        s[kb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, qf[0][1], s[kb][0], 0, 0, 0);
+        s[kb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, qf[1][1], s[kb][1], 0, 0, 0);
+      }
+    }
+    // ---- mask keys >= N (last tile only)
+    if (kt * 64 + 64 > N) {
+#pragma unroll
+      for (int kb = 0; kb < 4; kb++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          int key = kt * 64 + kb * 16 + 4 * g + i;
+          if (key >= N) { s[kb][0][i] = -INFINITY; s[kb][1][i] = -INFINITY; }
+        }
+    }
+    if constexpr (F32) {
+      // ---- exact online softmax per query column
+#pragma unroll
+      for (int qs = 0; qs < 2; qs++) {
+        f32x4 col[4] = {s[0][qs], s[1][qs], s[2][qs], s[3][qs]};
+        float mx = xmax4(max16(col));
+        float mnew = fmaxf(mrow[qs], mx);
+        float alpha = fexp2(mrow[qs] - mnew);
+        float sum = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 4; kb++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) { float p = fexp2(s[kb][qs][i] - mnew); s[kb][qs][i] = p; sum += p; }
+        lrow[qs] = lrow[qs] * alpha + xsum4(sum);
+        mrow[qs] = mnew;
+#pragma unroll
+        for (int ds = 0; ds < 4; ds++) o[ds][qs] *= alpha;
+      }
+#pragma unroll
+      for (int kb = 0; kb < 4; kb++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          int key = kb * 16 + 4 * g + i;
+#pragma unroll
+          for (int ds = 0; ds < 4; ds++) {
+            float a = *(const float*)(vs + L::vrow(key, (ds * 16 + li) * 4));
+            o[ds][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, s[kb][0][i], o[ds][0], 0, 0, 0);
+            o[ds][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, s[kb][1][i], o[ds][1], 0, 0, 0);
+          }
+        }
+    } else {
+      // ---- lazy max: s already holds score - m.  The first tile sets m exactly; later tiles only
+      // rescale when a score exceeds m by more than RESCALE_TH (wave-uniform branch).
+      float lm0 = 0.f, lm1 = 0.f;
+      if (!FAST || kt == 0) {
+        f32x4 c0[4] = {s[0][0], s[1][0], s[2][0], s[3][0]}, c1[4] = {s[0][1], s[1][1], s[2][1], s[3][1]};
+        lm0 = max16(c0); lm1 = max16(c1);
+      }
+      if (kt == 0 || (!FAST && __any(fmaxf(lm0, lm1) > RESCALE_TH))) {
+        float lmq[2] = {lm0, lm1};
+#pragma unroll
+        for (int qs = 0; qs < 2; qs++) {
+          float d = xmax4(lmq[qs]);
+          d = kt == 0 ? d : fmaxf(d, 0.f);
+          mrow[qs] = kt == 0 ? d : mrow[qs] + d;
+          float alpha = kt == 0 ? 1.f : fexp2(-d);
+#pragma unroll
+          for (int kb = 0; kb < 4; kb++) s[kb][qs] -= d;
+#pragma unroll
+          for (int ds = 0; ds < 4; ds++) o[ds][qs] *= alpha;
+          lacc[qs] *= alpha;
+          negm[qs] = f32x4{-mrow[qs], -mrow[qs], -mrow[qs], -mrow[qs]};
+        }
+      }
+      // ---- P = exp2(s); O^T += V^T P^T ; l += 1^T P^T
+      typedef __attribute__((address_space(3))) s16x4 lds_s4;
+      bf16x8 ones;
+#pragma unroll
+      for (int e = 0; e < 8; e++) ones[e] = (bf16)1.f;
+#pragma unroll
+      for (int kst = 0; kst < 2; kst++) {
+        bf16x8 pb[2];
+#pragma unroll
+        for (int qs = 0; qs < 2; qs++)
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            pb[qs][i] = (bf16)fexp2(s[2 * kst][qs][i]);
+            pb[qs][4 + i] = (bf16)fexp2(s[2 * kst + 1][qs][i]);
+          }
+        const int q = li >> 2, p = li & 3;
+#pragma unroll
+        for (int ds = 0; ds < 4; ds++) {
+          int byte = (ds * 16 + 4 * p) * 2;
+          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(vs + L::vrow(32 * kst + 4 * g + q, byte)));
+          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(vs + L::vrow(32 * kst + 16 + 4 * g + q, byte)));
+          bf16x4 a0 = __builtin_bit_cast(bf16x4, lo), a1 = __builtin_bit_cast(bf16x4, hi);
+          bf16x8 a = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+          o[ds][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb[0], o[ds][0], 0, 0, 0);
+          o[ds][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb[1], o[ds][1], 0, 0, 0);
+        }
+        lacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[0], lacc[0], 0, 0, 0);
+        lacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[1], lacc[1], 0, 0, 0);
+      }
+    }
+    }
+  };
+    // piece p = 4 wave + i of a tile: K pieces 0..7 (waves 0, 1), V pieces 8..15 (waves 2, 3); piece p & 7 holds keys
+    // 8 (p & 7) .. +7, lane l writes physical 16-B chunk l & 7 of key 8 (p & 7) + (l >> 3), i.e. the logical chunk the
+    // TileL swizzle puts there (K: 16-B chunks XOR (key >> 1) & 7; V: 32-B slots XOR (key >> 1) & 3)
+    const int wv = __builtin_amdgcn_readfirstlane(wave);     // wave-uniform: the descriptor and M0 stay scalar
+    unsigned dvo[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int pp = (wv & 1) * 4 + i, key = 8 * pp + (lane >> 3), c = lane & 7;
+      const int lc = wv < 2 ? (c ^ ((key >> 1) & 7)) : ((((c >> 1) ^ ((key >> 1) & 3)) << 1) | (c & 1));
+      dvo[i] = (unsigned)(key * 128 + lc * 16);
+    }
+    const char* src = (const char*)(wv < 2 ? Kp : Vp);
+    const int dsto = (wv < 2 ? 0 : L::BYTES) + (wv & 1) * 4096;
+    auto dma = [&](int kt, char* stage) {
+      // the descriptor rebased on the tile's first key (scalar work): keys >= N read zeros by the range check
+      const long off = (long)kt * 64 * 128;
+      const auto r = attn_rsrc(src + off, (unsigned long)N * 128 - off);
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(stage + dsto + i * 1024), 16, dvo[i], 0, 0, 0);
+    };
+    dma(0, smem);
+    vm_drain();
+    __syncthreads();
+    // unrolled by two so the stages are compile-time offsets; __restrict__ stage pointers let the wait-count pass see
+    // that this tile's LDS reads cannot alias the next tile's DMA (as in the backward kernels)
+    auto tile = [&](int kt, char* __restrict__ nxt, const char* __restrict__ cs) {
+      if (kt + 1 < nkt) dma(kt + 1, nxt);
+      tile_compute(kt, cs, cs + L::BYTES);
+      vm_drain();           // this wave's pieces of the next tile landed ...
+      __syncthreads();      // ... and every wave's; every wave done with this stage
+    };
+    int kt = 0;
+    for (; kt + 1 < nkt; kt += 2) { tile(kt, smem1, smem); tile(kt + 1, smem, smem1); }
+    if (kt < nkt) tile(kt, smem1, smem);
+  } else {
   Stage<T> stg;
   const int nkt = (N + 63) / 64;
   const auto rk = attn_rsrc(Kp, (unsigned long)N * 64 * sizeof(T)), rv = attn_rsrc(Vp, (unsigned long)N * 64 * sizeof(T));
@@ -303,6 +470,7 @@ __global__ void __launch_bounds__(256, 3) attn_fwd_kernel(const T* __restrict__ 
     if (more) stg.store(smem + (cur ^ 1) * 2 * L::BYTES, smem + (cur ^ 1) * 2 * L::BYTES + L::BYTES, tid);
     __syncthreads();
     cur ^= 1;
+  }
   }
   };
   if constexpr (!F32) {
@@ -1208,6 +1376,7 @@ __global__ void __launch_bounds__(64 * W) attn_bwd_dq32_kernel(const bf16* __res
 }
 
 // (hipcc 7.2 left the host stubs of these instances undefined when they were only named in the launcher below)
+template __global__ void attn_fwd_kernel<bf16, true>(const bf16*, const bf16*, const bf16*, bf16*, float*, int, int, int);
 template __global__ void attn_bwd_dq32_kernel<4>(const bf16*, const bf16*, const bf16*, const bf16*, const float*, const float*, bf16*,
                                                  int, int, QkvSink);
 template __global__ void attn_bwd_dkdv32_kernel<4>(const bf16*, const bf16*, const bf16*, const bf16*, const float*, const float*, bf16*,
@@ -1220,6 +1389,13 @@ int s3od_attn_fwd(int dtype, const void* q, const void* k, const void* v, void* 
   dim3 grid(cdiv(N, 128), B * H);
   // bf16 and f32: the 16x16 kernel (a 32x32x16 bf16 variant measured 6-8 % slower: 1083 -> 1150 us at bs 16, N 4101;
   // 3532 -> 3817 us at bs 4, N 16389, same box -- its extra row-sum MFMAs cost 2x the cycles; removed)
+  // bf16: K / V by LDS-DMA -- same box, one process, alternating: 902 -> 739 us at bs 16 N 4101, 3374 -> 2805 us at
+  // bs 4 N 16389, outputs bit-identical (profiles/r06k_attn_fwd_dma_ab.txt); S3OD_ATTN_DMA=0: the register-staged form
+  if (dtype == S3OD_BF16 && S3OD_KNOB("S3OD_ATTN_DMA", 1)) {
+    hipLaunchKernelGGL((attn_fwd_kernel<bf16, true>), grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)q, (const bf16*)k,
+                       (const bf16*)v, (bf16*)o, lse, N, H, S3OD_KNOB("S3OD_ATTN_FAST", 1));
+    return s3od_check_launch("attn_fwd");
+  }
   DISPATCH_T(dtype, {
     hipLaunchKernelGGL(attn_fwd_kernel<T>, grid, dim3(256), 0, (hipStream_t)stream, (const T*)q, (const T*)k, (const T*)v, (T*)o, lse, N, H,
                        S3OD_KNOB("S3OD_ATTN_FAST", 1));   // 0: the lazy-rescale loop throughout (A/B)

@@ -178,3 +178,35 @@ def test_attention_fwd_fixed_max_overflow_falls_back(case):
     assert float((got - ref).norm() / ref.norm()) < 1e-2
     assert float((got[:, 5] - ref[:, 5]).abs().max()) < 2e-2          # the planted row: ~ v[700]
     assert float((lse2 / LOG2E - torch.logsumexp(s, -1)).abs().max()) < 2e-2
+
+
+@pytest.mark.parametrize("N", [1, 63, 64, 65, 200, 1000, 4101])
+def test_attention_fwd_dma_staging_bit_identical(N, monkeypatch):
+    """The bf16 forward's LDS-DMA K / V staging (default) against the register-staged form (S3OD_ATTN_DMA=0): the same
+    tile images, the same MFMA chain, so O and LSE must match bit for bit -- ragged lengths cover a partial last key
+    tile (range-checked zeros past N), a single tile, an odd tile count (the unrolled-by-two loop's remainder) and the
+    partial last 128-query block."""
+    from s3od_amd._lib import lib, stream, BF16
+    B, H = 2, 3
+    g = torch.Generator(device="cuda").manual_seed(N)
+    q = (torch.randn(B * H, N, 64, device="cuda", generator=g) * 0.5).bfloat16()
+    k = torch.randn(B * H, N, 64, device="cuda", generator=g).bfloat16()
+    v = torch.randn(B * H, N, 64, device="cuda", generator=g).bfloat16()
+    outs = []
+    for dma in ("1", "0"):
+        monkeypatch.setenv("S3OD_ATTN_DMA", dma)          # read per call: tests/conftest.py sets S3OD_AB=1
+        o = torch.full((B, N, H * 64), float("nan"), device="cuda", dtype=torch.bfloat16)
+        lse = torch.full((B * H, N), float("nan"), device="cuda")
+        lib()("s3od_attn_fwd", BF16, q, k, v, o, lse, B, H, N, stream())
+        torch.cuda.synchronize()
+        outs.append((o, lse))
+    (o1, l1), (o0, l0) = outs
+    assert torch.isfinite(o1.float()).all() and torch.isfinite(l1).all()
+    assert torch.equal(o1, o0) and torch.equal(l1, l0)
+    # and against fp32 softmax of the same operands (natural-log LSE = lse2 / log2 e)
+    qe = q.float() / (LOG2E * 0.125)
+    s = torch.matmul(qe, k.float().transpose(1, 2)) * 0.125
+    ref = torch.matmul(torch.softmax(s, -1), v.float())
+    got = o1.view(B, N, H, 64).permute(0, 2, 1, 3).reshape(B * H, N, 64).float()
+    assert float((got - ref).norm() / ref.norm()) < 1e-2
+    assert float((l1 / LOG2E - torch.logsumexp(s, -1)).abs().max()) < 2e-2
