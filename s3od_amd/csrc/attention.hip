@@ -1067,17 +1067,34 @@ DEV void qkv_sink32(const QkvSink& o, int which, int b, int hh, int H, int tok0,
                     float scale, float (&csum)[2]) {
   const int h = lane >> 5, c = lane & 31;
   T* base = (T*)o.dqkv + (long)which * H * 64 + hh * 64;
+  // the RoPE table entries of all 16 rows are loaded before the first store (identity for prefix tokens, v and rows
+  // past N): read row by row, every row's loads waited behind the previous row's stores (one vmcnt counts both), 16
+  // serialized round trips at the end of every wave
+  // (unconditional loads from a clamped row, then selects: a conditional load became a branchy loop and the
+  // wait-count pass put a vmcnt(0) before every row's stores again)
+  float c0[16], c1[16], s0[16], s1[16];
+  const bool rq = which < 2 && o.P > 0;      // wave-uniform
+  if (rq) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int tok = tok0 + acc_row(i, h);
+      const bool rope = tok < N && tok >= N - o.P;
+      const long tp = rope ? (long)(tok - (N - o.P)) * 64 : 0;
+      const float a = o.cs[tp + c], bb = o.cs[tp + c + 32], d = o.sn[tp + c], e = o.sn[tp + c + 32];
+      c0[i] = rope ? a : 1.f;
+      c1[i] = rope ? bb : 1.f;
+      s0[i] = rope ? d : 0.f;
+      s1[i] = rope ? e : 0.f;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 16; i++) {
     const int tok = tok0 + acc_row(i, h);
     if (tok >= N) continue;
     float out[2] = {val[0][i] * scale, val[1][i] * scale};
-    if (which < 2 && tok >= N - o.P) {
-      const int tp = tok - (N - o.P);
-      const float* cs = o.cs + (long)tp * 64;
-      const float* sn = o.sn + (long)tp * 64;
-      out[0] = (cs[c] * val[0][i] + sn[c + 32] * val[1][i]) * scale;
-      out[1] = (cs[c + 32] * val[1][i] - sn[c] * val[0][i]) * scale;
+    if (rq) {
+      out[0] = (c0[i] * val[0][i] + s1[i] * val[1][i]) * scale;
+      out[1] = (c1[i] * val[1][i] - s0[i] * val[0][i]) * scale;
     }
     T* row = base + ((long)b * N + tok) * (3L * H * 64);
 #pragma unroll
