@@ -106,6 +106,23 @@ DEV float gelu_fast_grad(float x) {
   return 0.5f * (1.0f + f) + x * (0.39894228040143268f * e);
 }
 
+// 8 consecutive elements held raw (16 B for bf16, 32 B for f32) until they are consumed
+template <typename T> struct Row8;
+template <> struct Row8<float> {
+  float4 a, b;
+  DEV void load(const float* p) { a = ((const float4*)p)[0]; b = ((const float4*)p)[1]; }
+  DEV void get(float* v) const { v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w; }
+};
+template <> struct Row8<bf16> {
+  uint4 u;
+  DEV void load(const bf16* p) { u = *(const uint4*)p; }
+  DEV void get(float* v) const {
+    const bf16x8 x = __builtin_bit_cast(bf16x8, u);
+#pragma unroll
+    for (int e = 0; e < 8; e++) v[e] = (float)x[e];
+  }
+};
+
 // Dispatch / dev knobs (A/B switches and micro-benchmark sweeps; the defaults are the product path).
 // S3OD_KNOB(name, def) reads the environment ONCE, on the first call through that site, into a function-local
 // static; the per-call path never calls getenv.  S3OD_AB=1 (itself read once) re-reads every knob on every call,

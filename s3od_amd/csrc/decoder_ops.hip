@@ -268,17 +268,37 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const T* __restrict__
     }
     store8<T>(dz + o, out);
   };
+  // software-pipelined over 4-row batches: batch k+1's loads are issued before batch k's stores.  One vmcnt counts
+  // loads and stores in issue order, so a batch loaded AFTER the previous batch's stores waited for those stores too.
   long p = p0 + ri;
-  for (; p + 3 * rows < p1; p += 4 * rows) {
-    float d[4][8], zz[4][8], yy[4][8];
+  if (p + 3 * rows < p1) {
+    Row8<T> cd[4], cz[4], cy[4];
+    auto ld4 = [&](long pp, Row8<T> (&rd)[4], Row8<T> (&rz)[4], Row8<T> (&ry)[4]) {
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const long o = (p + j * rows) * C + c;
-      load8<T>(dy + o, d[j]); load8<T>(z + o, zz[j]);
-      rl.load(o, yy[j]);
+      for (int j = 0; j < 4; j++) {
+        const long o = (pp + j * rows) * C + c;
+        rd[j].load(dy + o); rz[j].load(z + o);
+        if (MODE == 1) ry[j].load(y_relu + o);
+      }
+    };
+    ld4(p, cd, cz, cy);
+    for (;;) {
+      const long pn = p + 4 * rows;
+      const bool more = pn + 3 * rows < p1;
+      Row8<T> nd[4], nz[4], ny[4];
+      if (more) ld4(pn, nd, nz, ny);
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        float d[8], zz[8], yy[8];
+        cd[j].get(d); cz[j].get(zz);
+        if (MODE == 1) cy[j].get(yy);
+        body((p + j * rows) * C + c, d, zz, yy);
+      }
+      p = pn;
+      if (!more) break;
+#pragma unroll
+      for (int j = 0; j < 4; j++) { cd[j] = nd[j]; cz[j] = nz[j]; cy[j] = ny[j]; }
     }
-#pragma unroll
-    for (int j = 0; j < 4; j++) body((p + j * rows) * C + c, d[j], zz[j], yy[j]);
   }
   for (; p < p1; p += rows) {
     float d[8], zz[8], yy[8];

@@ -851,23 +851,6 @@ template <class F> DEV void for_segments(const float* ct, int LDT, int BM, int B
   }
 }
 
-// 8 consecutive elements held raw (16 B for bf16, 32 B for f32) until they are consumed
-template <typename T> struct Row8;
-template <> struct Row8<float> {
-  float4 a, b;
-  DEV void load(const float* p) { a = ((const float4*)p)[0]; b = ((const float4*)p)[1]; }
-  DEV void get(float* v) const { v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w; }
-};
-template <> struct Row8<bf16> {
-  uint4 u;
-  DEV void load(const bf16* p) { u = *(const uint4*)p; }
-  DEV void get(float* v) const {
-    const bf16x8 x = __builtin_bit_cast(bf16x8, u);
-#pragma unroll
-    for (int e = 0; e < 8; e++) v[e] = (float)x[e];
-  }
-};
-
 // ------------------------------------------------------------------ common epilogue
 // out = act(acc*scale[n] + shift[n]) + res1 + res2 ; optional raw store (pre-act) and BN
 // batch statistics (sum / sum of squares of the pre-activation value, fp64 atomics).
